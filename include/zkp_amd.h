@@ -1,0 +1,120 @@
+/*
+ * zkp_amd.h — C ABI of libzkp_amd.so, the MI355X-native Groth16 prover that is a
+ * drop-in for the snarkjs `groth16.prove(zkey, wtns)` hot path of ZKP2P.
+ *
+ * Reference interface replaced (paths relative to the reference repo):
+ *   - CLI  `snarkjs groth16 prove <zkey> <wtns> <proof.json> <public.json>`
+ *          dizkus-scripts/5_gen_proof.sh:8, circuit/scripts/generate_proof_groth16.sh:11,
+ *          and its rapidsnark twin dizkus-scripts/6_gen_proof_rapidsnark.sh:26,
+ *          circuit/server-scripts/generate_proof.sh:5
+ *   - JS   `snarkjs.groth16.fullProve(input, wasm, zkey)` -> groth16.prove(zkey, wtns)
+ *          app/src/helpers/zkp.ts:94  (snarkjs@0.4.22, package-lock.json:3884-3896)
+ * The N-API addon (zk-p2p-onramp_amd/js/) binds exactly these entry points; see
+ * INTEGRATION.md for the binding a maintainer adds on the reference side.
+ *
+ * Conventions: plain pointers and sizes, no exceptions across the ABI, status codes
+ * plus a thread-local message (zkp_last_error).  All field values cross the ABI as
+ * 32-byte little-endian integers in STANDARD (non-Montgomery) form, exactly the
+ * bytes snarkjs writes as decimal strings in proof.json / public.json.
+ */
+#ifndef ZKP_AMD_H
+#define ZKP_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum zkp_status {
+  ZKP_OK = 0,
+  ZKP_ERR_INVALID_ARG = 1,     /* null pointer / bad size                                   */
+  ZKP_ERR_IO = 2,              /* file open/read/write failure                              */
+  ZKP_ERR_FORMAT = 3,          /* bad magic, version or section layout (binfileutils)      */
+  ZKP_ERR_PROTOCOL = 4,        /* zkey is not groth16   (snarkjs: "zkey file is not groth16") */
+  ZKP_ERR_CURVE = 5,           /* field mismatch        (snarkjs: "Curve of the witness does not match the curve of the proving key") */
+  ZKP_ERR_WITNESS_LENGTH = 6,  /* nWitness != nVars     (snarkjs: "Invalid witness length") */
+  ZKP_ERR_DEVICE = 7,          /* HIP runtime error / no usable MI355X                     */
+  ZKP_ERR_OUT_OF_MEMORY = 8,
+  ZKP_ERR_INTERNAL = 9
+} zkp_status;
+
+/* Opaque prover handle: parsed + validated zkey whose point sections are resident in
+ * HBM of every device in the list (uploaded once at load).  Immutable after load;
+ * concurrent zkp_prove calls on one handle are safe (serialised per device). */
+typedef struct zkp_prover zkp_prover;
+
+/* One Groth16 proof: affine coordinates, standard-form LE (the pi_a/pi_b/pi_c of
+ * proof.json without the projective "1"/["1","0"] tails).  public_signals is a
+ * caller-owned buffer of public_capacity * 32 bytes receiving w[1..nPublic]. */
+typedef struct zkp_proof {
+  uint8_t pi_a[2][32];    /* x, y                              */
+  uint8_t pi_b[2][2][32]; /* [x.c0, x.c1], [y.c0, y.c1]        */
+  uint8_t pi_c[2][32];    /* x, y                              */
+  uint32_t n_public;      /* set by zkp_prove                  */
+  uint32_t public_capacity;
+  uint8_t* public_signals;
+} zkp_proof;
+
+/* Load a .zkey (snarkjs groth16, version 1) from a path or a memory buffer.
+ * devices: HIP device ordinals (NULL/0 -> device 0).  Every device gets a full
+ * resident copy (batch mode: proofs are spread over devices by zkp_prove_batch). */
+zkp_status zkp_prover_load_file(const char* zkey_path, const int* devices, int ndev, zkp_prover** out);
+zkp_status zkp_prover_load_mem(const uint8_t* zkey, size_t len, const int* devices, int ndev, zkp_prover** out);
+
+zkp_status zkp_prover_info(const zkp_prover* p, uint32_t* n_vars, uint32_t* n_public, uint32_t* domain_size);
+
+/* Prove one witness (.wtns bytes, version <= 2).  r32 / s32: 32-byte LE blinding
+ * scalars (< r); NULL -> drawn from the OS CSPRNG (production).  Non-NULL is for
+ * bit-exact tests: A, B, C are then a deterministic function of (zkey, wtns, r, s). */
+zkp_status zkp_prove(zkp_prover* p, const uint8_t* wtns, size_t len, const uint8_t* r32, const uint8_t* s32,
+                     zkp_proof* out);
+
+/* Prove n witnesses, spread over the prover's devices (one host worker per device).
+ * r32s / s32s may be NULL (all random) or arrays of n pointers. */
+zkp_status zkp_prove_batch(zkp_prover* p, const uint8_t* const* wtns, const size_t* lens, int n,
+                           const uint8_t* const* r32s, const uint8_t* const* s32s, zkp_proof* outs);
+
+/* CLI-equivalent: `groth16 prove <zkey> <wtns> <proof.json> <public.json>` on a
+ * loaded prover; writes JSON byte-compatible with snarkjs (JSON.stringify(x,null,1)). */
+zkp_status zkp_prove_files(zkp_prover* p, const char* wtns_path, const char* proof_json_path,
+                           const char* public_json_path);
+
+/* Format a proof as snarkjs proof.json / public.json text.  Returns the needed size
+ * (including NUL) in *needed; writes when cap is large enough. */
+zkp_status zkp_proof_json(const zkp_proof* proof, char* buf, size_t cap, size_t* needed);
+zkp_status zkp_public_json(const zkp_proof* proof, char* buf, size_t cap, size_t* needed);
+
+/* Per-stage device timings (ms) of the last zkp_prove on this handle:
+ * [0] wtns H2D, [1] buildABC, [2] NTT/quotient, [3] MSM G1 (A,B1,C,H), [4] MSM G2 (B2),
+ * [5] host assembly, [6] total wall.  n = capacity of ms. */
+zkp_status zkp_prover_timings(const zkp_prover* p, float* ms, int n);
+
+void zkp_prover_free(zkp_prover* p);
+
+/* Thread-local message of the last failing call on this thread ("" if none). */
+const char* zkp_last_error(void);
+
+/* Library / build identification, e.g. "zkp_amd 0.1 gfx950". */
+const char* zkp_version(void);
+
+/* ---- kernel-level entry points (tests and benchmarks; same kernels as zkp_prove) ----
+ * points: zkey layout (affine, Montgomery 2^256 LE; infinity = zero bytes),
+ * scalars: 32-byte LE standard form.  out: affine standard-form LE (64 / 128 bytes),
+ * all-zero + *is_inf = 1 for the point at infinity. */
+zkp_status zkp_msm_g1(int device, const uint8_t* points, const uint8_t* scalars, size_t n, uint8_t* out64,
+                      int* is_inf);
+zkp_status zkp_msm_g2(int device, const uint8_t* points, const uint8_t* scalars, size_t n, uint8_t* out128,
+                      int* is_inf);
+/* In-place Fr transforms on n = 2^k standard-form LE elements, natural order:
+ * mode 0: forward (A_j = sum a_i w^ij), 1: inverse, 2: coset-extend (snarkjs
+ * ifft -> batchApplyKey(1, Fr.w[k+1]) -> fft). */
+zkp_status zkp_ntt_fr(int device, uint8_t* data, size_t n, int mode);
+/* The H-MSM scalars P_j (standard form, n = domain) for (zkey, wtns): rows A4..A8. */
+zkp_status zkp_quotient(zkp_prover* p, const uint8_t* wtns, size_t len, uint8_t* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ZKP_AMD_H */

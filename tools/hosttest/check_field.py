@@ -1,0 +1,78 @@
+#!/usr/bin/env python3
+"""Drive tools/hosttest/field_host (device field/curve code compiled for the host)
+with random inputs and compare against the Python oracle."""
+import os, random, subprocess, sys
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", ".."))
+from oracle import bn254
+P, R = bn254.P, bn254.R
+RP = 1 << 261
+BIN = os.path.join(os.path.dirname(__file__), "field_host")
+
+def w8(x): return " ".join("%x" % ((x >> (32 * i)) & 0xffffffff) for i in range(8))
+def p8(s): return sum(int(t, 16) << (32 * i) for i, t in enumerate(s.split()[:8]))
+
+def main(n=300):
+    rnd = random.Random(1)
+    lines, checks = [], []
+    inv_rp_p = pow(RP, -1, P); inv_rp_r = pow(RP, -1, R)
+    for _ in range(n):
+        a, b = rnd.randrange(2 * P), rnd.randrange(2 * P)
+        lines.append("mulq %s %s" % (w8(a), w8(b))); checks.append(("mulq", lambda v, a=a, b=b: v % P == a * b * inv_rp_p % P and v < 2 * P))
+        lines.append("sqrq %s" % w8(a)); checks.append(("sqrq", lambda v, a=a: v % P == a * a * inv_rp_p % P and v < 2 * P))
+        lines.append("addq %s %s" % (w8(a), w8(b))); checks.append(("addq", lambda v, a=a, b=b: v % P == (a + b) % P and v < 2 * P))
+        lines.append("subq %s %s" % (w8(a), w8(b))); checks.append(("subq", lambda v, a=a, b=b: v % P == (a - b) % P and v < 2 * P))
+        lines.append("canonq %s" % w8(a)); checks.append(("canonq", lambda v, a=a: v == a % P))
+        x, y = rnd.randrange(2 * R), rnd.randrange(2 * R)
+        lines.append("mulr %s %s" % (w8(x), w8(y))); checks.append(("mulr", lambda v, x=x, y=y: v % R == x * y * inv_rp_r % R and v < 2 * R))
+    for z in (0, P):
+        lines.append("iszq %s" % w8(z)); checks.append(("iszq", lambda v: v == 1))
+    out = subprocess.run([BIN], input="\n".join(lines) + "\n", capture_output=True, text=True).stdout.strip().split("\n")
+    bad = {}
+    for (name, fn), o in zip(checks, out):
+        v = int(o) if name == "iszq" else p8(o)
+        if not fn(v):
+            bad[name] = bad.get(name, 0) + 1
+    print("checked", len(checks), "bad", bad)
+    return not bad
+
+if __name__ == "__main__":
+    sys.exit(0 if main() else 1)
+
+def curve_check(n=40):
+    rnd = random.Random(2)
+    inv_rp = pow(RP, -1, P)
+    dev = lambda x: x * RP % P
+    undev = lambda v: v * inv_rp % P
+    lines, exp = [], []
+    for i in range(n):
+        p = bn254.g1_mul(bn254.G1_GEN, rnd.randrange(1, R))
+        q = bn254.g1_mul(bn254.G1_GEN, rnd.randrange(1, R)) if i % 4 else p
+        if i % 7 == 3:
+            q = bn254.g1_neg(p)
+        lines.append("g1add %s %s %s %s" % (w8(dev(p[0])), w8(dev(p[1])), w8(dev(q[0])), w8(dev(q[1]))))
+        exp.append(("add", bn254.g1_add(p, q)))
+        lines.append("g1addx %s %s %s %s" % (w8(dev(p[0])), w8(dev(p[1])), w8(dev(q[0])), w8(dev(q[1]))))
+        exp.append(("addx", bn254.g1_add(p, bn254.g1_add(q, q))))
+        z = rnd.randrange(P)
+        lines.append("conv %s" % w8(z * (1 << 256) % P)); exp.append(("conv", z))
+    out = subprocess.run([BIN], input="\n".join(lines) + "\n", capture_output=True, text=True).stdout.strip().split("\n")
+    bad = 0
+    for (kind, e), o in zip(exp, out):
+        t = o.split()
+        if kind == "conv":
+            ok = undev(p8(" ".join(t[:8]))) == e
+        else:
+            X, Y, ZZ, ZZZ = [undev(p8(" ".join(t[8 * k:8 * k + 8]))) for k in range(4)]
+            if ZZ == 0:
+                got = None
+            else:
+                got = (X * pow(ZZ, -1, P) % P, Y * pow(ZZZ, -1, P) % P)
+            ok = got == e
+        if not ok:
+            bad += 1
+            print("BAD", kind)
+    print("curve checked", len(exp), "bad", bad)
+    return bad == 0
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "curve":
+    sys.exit(0 if curve_check() else 1)

@@ -1,0 +1,45 @@
+// Host-side check of the device field/curve code (field.hpp, curve.hpp are
+// __host__ __device__): reads ops from stdin, prints results, compared by
+// tools/hosttest/check_field.py against the Python oracle.
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include "../../zk-p2p-onramp_amd/csrc/curve.hpp"
+using namespace zkp;
+
+static void rd(uint32_t w[8]) { for (int i = 0; i < 8; ++i) if (scanf("%x", &w[i]) != 1) exit(1); }
+static void pr(const uint32_t w[8]) { for (int i = 0; i < 8; ++i) printf("%08x ", w[i]); }
+template <class C> static Fe<C> rdf() { uint32_t w[8]; rd(w); return unpack<C>(w); }
+template <class C> static void prf(const Fe<C>& x) { uint32_t w[8]; pack(x, w); pr(w); }
+
+int main() {
+  char op[32];
+  while (scanf("%31s", op) == 1) {
+    std::string o(op);
+    if (o == "mulq") { Fq a = rdf<FqCfg>(), b = rdf<FqCfg>(); prf(mul(a, b)); }
+    else if (o == "sqrq") { Fq a = rdf<FqCfg>(); prf(sqr(a)); }
+    else if (o == "addq") { Fq a = rdf<FqCfg>(), b = rdf<FqCfg>(); prf(add(a, b)); }
+    else if (o == "subq") { Fq a = rdf<FqCfg>(), b = rdf<FqCfg>(); prf(sub(a, b)); }
+    else if (o == "mulr") { Fr a = rdf<FrCfg>(), b = rdf<FrCfg>(); prf(mul(a, b)); }
+    else if (o == "canonq") { Fq a = rdf<FqCfg>(); prf(canon(a)); }
+    else if (o == "iszq") { Fq a = rdf<FqCfg>(); printf("%d", (int)is_zero(a)); }
+    else if (o == "conv") { Fq a = rdf<FqCfg>(); prf(mul(a, fe_const<FqCfg>(Conv::FQ_ZKEY_TO_DEV))); }
+    else if (o == "g1add") {  // acc(affine) + q(affine) via xyzz, output xyzz packed
+      Aff<Fq> p{rdf<FqCfg>(), rdf<FqCfg>()}, q{rdf<FqCfg>(), rdf<FqCfg>()};
+      Xyzz<Fq> acc = xyzz_inf<Fq>();
+      xyzz_add_aff(acc, p);
+      xyzz_add_aff(acc, q);
+      prf(acc.x); prf(acc.y); prf(acc.zz); prf(acc.zzz);
+    } else if (o == "g1addx") {  // xyzz + xyzz
+      Aff<Fq> p{rdf<FqCfg>(), rdf<FqCfg>()}, q{rdf<FqCfg>(), rdf<FqCfg>()};
+      Xyzz<Fq> a = xyzz_inf<Fq>(), b = xyzz_inf<Fq>();
+      xyzz_add_aff(a, p); xyzz_add_aff(b, q);
+      b = xyzz_dbl(b);
+      xyzz_add(a, b);
+      prf(a.x); prf(a.y); prf(a.zz); prf(a.zzz);
+    }
+    printf("\n");
+    fflush(stdout);
+  }
+  return 0;
+}

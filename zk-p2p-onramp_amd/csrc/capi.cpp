@@ -1,0 +1,218 @@
+// C ABI of libzkp_amd.so (include/zkp_amd.h).  Every entry point catches all C++
+// exceptions and turns them into a zkp_status plus a thread-local message.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/zkp_amd.h"
+#include "hip_check.hpp"
+#include "host_ec.hpp"
+#include "prover.hpp"
+
+struct zkp_prover {
+  zkp::Prover* impl;
+};
+
+namespace {
+
+thread_local std::string g_err;
+
+zkp_status fail(zkp_status s, const std::string& m) {
+  g_err = m;
+  return s;
+}
+
+template <class Fn>
+zkp_status guard(Fn&& fn) {
+  try {
+    g_err.clear();
+    fn();
+    return ZKP_OK;
+  } catch (const zkp::ZkpError& e) {
+    return fail(e.status, e.what());
+  } catch (const zkp::HipError& e) {
+    if (e.code == hipErrorOutOfMemory) return fail(ZKP_ERR_OUT_OF_MEMORY, e.what());
+    return fail(ZKP_ERR_DEVICE, e.what());
+  } catch (const std::bad_alloc&) {
+    return fail(ZKP_ERR_OUT_OF_MEMORY, "host out of memory");
+  } catch (const std::exception& e) {
+    return fail(ZKP_ERR_INTERNAL, e.what());
+  } catch (...) {
+    return fail(ZKP_ERR_INTERNAL, "unknown error");
+  }
+}
+
+std::vector<uint8_t> read_file(const char* path) {
+  std::ifstream f(path, std::ios::binary | std::ios::ate);
+  if (!f) throw zkp::ZkpError(ZKP_ERR_IO, std::string("cannot open ") + path);
+  const std::streamsize n = f.tellg();
+  f.seekg(0);
+  std::vector<uint8_t> buf((size_t)n);
+  if (n && !f.read(reinterpret_cast<char*>(buf.data()), n))
+    throw zkp::ZkpError(ZKP_ERR_IO, std::string("cannot read ") + path);
+  return buf;
+}
+
+std::string dec(const uint8_t* le32) { return zkp::host::u256_to_dec(zkp::host::u256_from_le(le32)); }
+
+// JSON.stringify(obj, null, 1) of snarkjs' proof object (key order pi_a, pi_b, pi_c, protocol, curve)
+std::string proof_json(const zkp_proof* p) {
+  std::string s = "{\n \"pi_a\": [\n  \"" + dec(p->pi_a[0]) + "\",\n  \"" + dec(p->pi_a[1]) + "\",\n  \"1\"\n ],\n";
+  s += " \"pi_b\": [\n  [\n   \"" + dec(p->pi_b[0][0]) + "\",\n   \"" + dec(p->pi_b[0][1]) + "\"\n  ],\n  [\n   \"" +
+       dec(p->pi_b[1][0]) + "\",\n   \"" + dec(p->pi_b[1][1]) + "\"\n  ],\n  [\n   \"1\",\n   \"0\"\n  ]\n ],\n";
+  s += " \"pi_c\": [\n  \"" + dec(p->pi_c[0]) + "\",\n  \"" + dec(p->pi_c[1]) + "\",\n  \"1\"\n ],\n";
+  s += " \"protocol\": \"groth16\",\n \"curve\": \"bn128\"\n}";
+  return s;
+}
+
+std::string public_json(const zkp_proof* p) {
+  const uint32_t n = std::min(p->n_public, p->public_capacity);
+  if (n == 0 || !p->public_signals) return "[]";
+  std::string s = "[\n";
+  for (uint32_t i = 0; i < n; ++i) {
+    s += " \"" + dec(p->public_signals + 32 * i) + "\"";
+    s += (i + 1 < n) ? ",\n" : "\n";
+  }
+  s += "]";
+  return s;
+}
+
+zkp_status emit(const std::string& s, char* buf, size_t cap, size_t* needed) {
+  if (needed) *needed = s.size() + 1;
+  if (buf && cap >= s.size() + 1) {
+    std::memcpy(buf, s.c_str(), s.size() + 1);
+    return ZKP_OK;
+  }
+  if (buf) return fail(ZKP_ERR_INVALID_ARG, "buffer too small");
+  return ZKP_OK;
+}
+
+void write_file(const char* path, const std::string& s) {
+  std::ofstream f(path, std::ios::binary);
+  if (!f || !f.write(s.data(), (std::streamsize)s.size())) throw zkp::ZkpError(ZKP_ERR_IO, std::string("cannot write ") + path);
+}
+
+std::vector<int> dev_list(const int* devices, int ndev) {
+  std::vector<int> v;
+  if (devices)
+    for (int i = 0; i < ndev; ++i) v.push_back(devices[i]);
+  return v;
+}
+
+}  // namespace
+
+extern "C" {
+
+zkp_status zkp_prover_load_mem(const uint8_t* zkey, size_t len, const int* devices, int ndev, zkp_prover** out) {
+  if (!zkey || !out || ndev < 0) return fail(ZKP_ERR_INVALID_ARG, "null argument");
+  *out = nullptr;
+  return guard([&] {
+    auto* h = new zkp_prover{nullptr};
+    try {
+      h->impl = new zkp::Prover(zkey, len, dev_list(devices, ndev));
+    } catch (...) {
+      delete h;
+      throw;
+    }
+    *out = h;
+  });
+}
+
+zkp_status zkp_prover_load_file(const char* path, const int* devices, int ndev, zkp_prover** out) {
+  if (!path || !out) return fail(ZKP_ERR_INVALID_ARG, "null argument");
+  std::vector<uint8_t> buf;
+  zkp_status s = guard([&] { buf = read_file(path); });
+  if (s != ZKP_OK) return s;
+  return zkp_prover_load_mem(buf.data(), buf.size(), devices, ndev, out);
+}
+
+zkp_status zkp_prover_info(const zkp_prover* p, uint32_t* n_vars, uint32_t* n_public, uint32_t* domain_size) {
+  if (!p) return fail(ZKP_ERR_INVALID_ARG, "null prover");
+  const auto& h = p->impl->header();
+  if (n_vars) *n_vars = h.n_vars;
+  if (n_public) *n_public = h.n_public;
+  if (domain_size) *domain_size = h.domain_size;
+  return ZKP_OK;
+}
+
+zkp_status zkp_prove(zkp_prover* p, const uint8_t* wtns, size_t len, const uint8_t* r32, const uint8_t* s32,
+                     zkp_proof* out) {
+  if (!p || !wtns || !out) return fail(ZKP_ERR_INVALID_ARG, "null argument");
+  return guard([&] { p->impl->prove(wtns, len, r32, s32, out); });
+}
+
+zkp_status zkp_prove_batch(zkp_prover* p, const uint8_t* const* wtns, const size_t* lens, int n,
+                           const uint8_t* const* r32s, const uint8_t* const* s32s, zkp_proof* outs) {
+  if (!p || (n > 0 && (!wtns || !lens || !outs)) || n < 0) return fail(ZKP_ERR_INVALID_ARG, "null argument");
+  return guard([&] { p->impl->prove_batch(wtns, lens, n, r32s, s32s, outs); });
+}
+
+zkp_status zkp_prove_files(zkp_prover* p, const char* wtns_path, const char* proof_path, const char* public_path) {
+  if (!p || !wtns_path || !proof_path || !public_path) return fail(ZKP_ERR_INVALID_ARG, "null argument");
+  return guard([&] {
+    std::vector<uint8_t> w = read_file(wtns_path);
+    const uint32_t npub = p->impl->header().n_public;
+    std::vector<uint8_t> pub((size_t)npub * 32 + 32);
+    zkp_proof pr{};
+    pr.public_capacity = npub;
+    pr.public_signals = pub.data();
+    p->impl->prove(w.data(), w.size(), nullptr, nullptr, &pr);
+    write_file(proof_path, proof_json(&pr));
+    write_file(public_path, public_json(&pr));
+  });
+}
+
+zkp_status zkp_proof_json(const zkp_proof* proof, char* buf, size_t cap, size_t* needed) {
+  if (!proof) return fail(ZKP_ERR_INVALID_ARG, "null proof");
+  return emit(proof_json(proof), buf, cap, needed);
+}
+
+zkp_status zkp_public_json(const zkp_proof* proof, char* buf, size_t cap, size_t* needed) {
+  if (!proof) return fail(ZKP_ERR_INVALID_ARG, "null proof");
+  return emit(public_json(proof), buf, cap, needed);
+}
+
+zkp_status zkp_prover_timings(const zkp_prover* p, float* ms, int n) {
+  if (!p || !ms) return fail(ZKP_ERR_INVALID_ARG, "null argument");
+  p->impl->timings(ms, n);
+  return ZKP_OK;
+}
+
+void zkp_prover_free(zkp_prover* p) {
+  if (!p) return;
+  delete p->impl;
+  delete p;
+}
+
+const char* zkp_last_error(void) { return g_err.c_str(); }
+
+const char* zkp_version(void) { return "zkp_amd 0.1 gfx950"; }
+
+zkp_status zkp_msm_g1(int device, const uint8_t* points, const uint8_t* scalars, size_t n, uint8_t* out64,
+                      int* is_inf) {
+  if ((n && (!points || !scalars)) || !out64 || !is_inf) return fail(ZKP_ERR_INVALID_ARG, "null argument");
+  return guard([&] { zkp::msm_points(device, zkp::Curve::G1, points, scalars, n, out64, is_inf); });
+}
+
+zkp_status zkp_msm_g2(int device, const uint8_t* points, const uint8_t* scalars, size_t n, uint8_t* out128,
+                      int* is_inf) {
+  if ((n && (!points || !scalars)) || !out128 || !is_inf) return fail(ZKP_ERR_INVALID_ARG, "null argument");
+  return guard([&] { zkp::msm_points(device, zkp::Curve::G2, points, scalars, n, out128, is_inf); });
+}
+
+zkp_status zkp_ntt_fr(int device, uint8_t* data, size_t n, int mode) {
+  if (!data || mode < 0 || mode > 2) return fail(ZKP_ERR_INVALID_ARG, "bad argument");
+  return guard([&] { zkp::ntt_fr(device, data, n, mode); });
+}
+
+zkp_status zkp_quotient(zkp_prover* p, const uint8_t* wtns, size_t len, uint8_t* out) {
+  if (!p || !wtns || !out) return fail(ZKP_ERR_INVALID_ARG, "null argument");
+  return guard([&] { p->impl->quotient(wtns, len, out); });
+}
+
+}  // extern "C"

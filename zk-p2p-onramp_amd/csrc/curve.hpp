@@ -1,0 +1,239 @@
+// BN254 G1 / G2 group arithmetic for gfx950 — device side.
+//
+// Buckets and partial sums use XYZZ coordinates (x = X/ZZ, y = Y/ZZZ,
+// ZZ^3 = ZZZ^2): a mixed add (XYZZ + affine) is 8M + 2S and needs no inversion
+// (hyperelliptic.org EFD "madd-2008-s"; full add "add-2008-s", doubling
+// "dbl-2008-s-1", affine doubling "mdbl-2008-s-1").  Infinity is ZZ == ZZZ == 0
+// held exactly (never produced by arithmetic on non-degenerate inputs).  Affine
+// infinity is (0, 0), which is off-curve, matching the zkey encoding of the
+// point at infinity as all-zero bytes.
+//
+// Every edge case (P == Q -> doubling, P == -Q -> infinity) is handled, so MSM
+// results are exact for any inputs (restating ffjavascript g1m/g2m add, A11).
+#pragma once
+#include "field.hpp"
+
+namespace zkp {
+
+template <class F>
+struct Aff {
+  F x, y;
+};
+
+template <class F>
+struct Xyzz {
+  F x, y, zz, zzz;
+};
+
+template <class F>
+ZDEV F f_zero();
+template <>
+ZDEV Fq f_zero<Fq>() { return fe_zero<FqCfg>(); }
+template <>
+ZDEV Fq2 f_zero<Fq2>() { return Fq2{fe_zero<FqCfg>(), fe_zero<FqCfg>()}; }
+
+template <class F>
+ZDEV F f_one();
+template <>
+ZDEV Fq f_one<Fq>() { return fe_one<FqCfg>(); }
+template <>
+ZDEV Fq2 f_one<Fq2>() { return Fq2{fe_one<FqCfg>(), fe_zero<FqCfg>()}; }
+
+template <class F>
+ZDEV Xyzz<F> xyzz_inf() {
+  Xyzz<F> r;
+  r.x = f_one<F>();
+  r.y = f_one<F>();
+  r.zz = f_zero<F>();
+  r.zzz = f_zero<F>();
+  return r;
+}
+
+template <class F>
+ZDEV bool xyzz_is_inf(const Xyzz<F>& p) { return is_zero_raw(p.zz); }
+
+template <class F>
+ZDEV bool aff_is_inf(const Aff<F>& p) { return is_zero_raw(p.x) && is_zero_raw(p.y); }
+
+template <class F>
+ZDEV Aff<F> aff_neg(const Aff<F>& p) {
+  Aff<F> r;
+  r.x = p.x;
+  r.y = sub(f_zero<F>(), p.y);
+  return r;
+}
+
+// 2 * (x, y), affine input (mdbl-2008-s-1)
+template <class F>
+ZDEV Xyzz<F> xyzz_dbl_aff(const Aff<F>& p) {
+  F U = dbl(p.y);
+  F V = sqr(U);
+  F W = mul(U, V);
+  F S = mul(p.x, V);
+  F X2 = sqr(p.x);
+  F M = add(dbl(X2), X2);
+  Xyzz<F> r;
+  r.x = sub(sqr(M), dbl(S));
+  r.y = sub(mul(M, sub(S, r.x)), mul(W, p.y));
+  r.zz = V;
+  r.zzz = W;
+  return r;
+}
+
+// 2 * P (dbl-2008-s-1, a = 0)
+template <class F>
+ZDEV Xyzz<F> xyzz_dbl(const Xyzz<F>& p) {
+  if (xyzz_is_inf(p)) return p;
+  F U = dbl(p.y);
+  F V = sqr(U);
+  F W = mul(U, V);
+  F S = mul(p.x, V);
+  F X2 = sqr(p.x);
+  F M = add(dbl(X2), X2);
+  Xyzz<F> r;
+  r.x = sub(sqr(M), dbl(S));
+  r.y = sub(mul(M, sub(S, r.x)), mul(W, p.y));
+  r.zz = mul(V, p.zz);
+  r.zzz = mul(W, p.zzz);
+  return r;
+}
+
+// acc += q (q affine, may be infinity)  — madd-2008-s
+template <class F>
+ZDEV void xyzz_add_aff(Xyzz<F>& acc, const Aff<F>& q) {
+  if (aff_is_inf(q)) return;
+  if (xyzz_is_inf(acc)) {
+    acc.x = q.x;
+    acc.y = q.y;
+    acc.zz = f_one<F>();
+    acc.zzz = f_one<F>();
+    return;
+  }
+  F U2 = mul(q.x, acc.zz);
+  F S2 = mul(q.y, acc.zzz);
+  F P = sub(U2, acc.x);
+  F R = sub(S2, acc.y);
+  if (is_zero(P)) {
+    if (is_zero(R))
+      acc = xyzz_dbl_aff(q);
+    else
+      acc = xyzz_inf<F>();
+    return;
+  }
+  F PP = sqr(P);
+  F PPP = mul(P, PP);
+  F Q = mul(acc.x, PP);
+  F X3 = sub(sub(sqr(R), PPP), dbl(Q));
+  F Y3 = sub(mul(R, sub(Q, X3)), mul(acc.y, PPP));
+  acc.zz = mul(acc.zz, PP);
+  acc.zzz = mul(acc.zzz, PPP);
+  acc.x = X3;
+  acc.y = Y3;
+}
+
+// acc += q (both XYZZ) — add-2008-s
+template <class F>
+ZDEV void xyzz_add(Xyzz<F>& acc, const Xyzz<F>& q) {
+  if (xyzz_is_inf(q)) return;
+  if (xyzz_is_inf(acc)) {
+    acc = q;
+    return;
+  }
+  F U1 = mul(acc.x, q.zz);
+  F U2 = mul(q.x, acc.zz);
+  F S1 = mul(acc.y, q.zzz);
+  F S2 = mul(q.y, acc.zzz);
+  F P = sub(U2, U1);
+  F R = sub(S2, S1);
+  if (is_zero(P)) {
+    if (is_zero(R))
+      acc = xyzz_dbl(acc);
+    else
+      acc = xyzz_inf<F>();
+    return;
+  }
+  F PP = sqr(P);
+  F PPP = mul(P, PP);
+  F Q = mul(U1, PP);
+  F X3 = sub(sub(sqr(R), PPP), dbl(Q));
+  F Y3 = sub(mul(R, sub(Q, X3)), mul(S1, PPP));
+  acc.zz = mul(mul(acc.zz, q.zz), PP);
+  acc.zzz = mul(mul(acc.zzz, q.zzz), PPP);
+  acc.x = X3;
+  acc.y = Y3;
+}
+
+template <class F>
+ZDEV Xyzz<F> xyzz_neg(const Xyzz<F>& p) {
+  Xyzz<F> r = p;
+  r.y = sub(f_zero<F>(), p.y);
+  return r;
+}
+
+// ---------------------------------------------------------------- storage (HBM) layouts
+// G1 affine: 16 words (x, y), each 8 LE words.  G2 affine: 32 words (x.c0, x.c1, y.c0, y.c1).
+// XYZZ: 4 coordinates in the same order.
+
+ZDEV void load_f(const uint32_t* p, Fq& x) { x = load_fe<FqCfg>(p); }
+ZDEV void load_f(const uint32_t* p, Fq2& x) {
+  x.c0 = load_fe<FqCfg>(p);
+  x.c1 = load_fe<FqCfg>(p + 8);
+}
+ZDEV void store_f(uint32_t* p, const Fq& x) { store_fe(p, x); }
+ZDEV void store_f(uint32_t* p, const Fq2& x) {
+  store_fe(p, x.c0);
+  store_fe(p + 8, x.c1);
+}
+
+template <class F>
+struct FWords;
+template <>
+struct FWords<Fq> {
+  static constexpr int W = 8;
+};
+template <>
+struct FWords<Fq2> {
+  static constexpr int W = 16;
+};
+
+template <class F>
+ZDEV Aff<F> load_aff(const uint32_t* base, size_t idx) {
+  constexpr int W = FWords<F>::W;
+  const uint32_t* p = base + idx * (2 * W);
+  Aff<F> r;
+  load_f(p, r.x);
+  load_f(p + W, r.y);
+  return r;
+}
+
+template <class F>
+ZDEV void store_aff(uint32_t* base, size_t idx, const Aff<F>& a) {
+  constexpr int W = FWords<F>::W;
+  uint32_t* p = base + idx * (2 * W);
+  store_f(p, a.x);
+  store_f(p + W, a.y);
+}
+
+template <class F>
+ZDEV Xyzz<F> load_xyzz(const uint32_t* base, size_t idx) {
+  constexpr int W = FWords<F>::W;
+  const uint32_t* p = base + idx * (4 * W);
+  Xyzz<F> r;
+  load_f(p, r.x);
+  load_f(p + W, r.y);
+  load_f(p + 2 * W, r.zz);
+  load_f(p + 3 * W, r.zzz);
+  return r;
+}
+
+template <class F>
+ZDEV void store_xyzz(uint32_t* base, size_t idx, const Xyzz<F>& a) {
+  constexpr int W = FWords<F>::W;
+  uint32_t* p = base + idx * (4 * W);
+  store_f(p, a.x);
+  store_f(p + W, a.y);
+  store_f(p + 2 * W, a.zz);
+  store_f(p + 3 * W, a.zzz);
+}
+
+}  // namespace zkp

@@ -1,0 +1,227 @@
+// Pippenger MSM engine for BN254 G1/G2 on gfx950.  See msm.hpp for the pipeline.
+#include "msm.hpp"
+
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <stdexcept>
+#include <string>
+
+#include "curve.hpp"
+#include "msm_kernels.hpp"
+#include "hip_check.hpp"
+
+namespace zkp {
+
+namespace {
+
+constexpr int TPB = 256;
+
+inline unsigned grid_for(size_t n, int tpb = TPB) { return (unsigned)((n + tpb - 1) / tpb); }
+
+__global__ __launch_bounds__(TPB) void k_digits(const uint32_t* __restrict__ scalars, uint32_t n, int c, int W,
+                                                uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+  msmk::digits(blockIdx.x * TPB + threadIdx.x, scalars, n, c, W, keys, vals);
+}
+__global__ __launch_bounds__(TPB) void k_bounds(const uint32_t* __restrict__ keys, uint32_t total,
+                                                uint32_t* __restrict__ start, uint32_t* __restrict__ end) {
+  msmk::bounds(blockIdx.x * TPB + threadIdx.x, keys, total, start, end);
+}
+__global__ __launch_bounds__(TPB) void k_task_counts(const uint32_t* __restrict__ start,
+                                                     const uint32_t* __restrict__ end, uint32_t nb, uint32_t S,
+                                                     uint32_t* __restrict__ cnt) {
+  msmk::task_counts(blockIdx.x * TPB + threadIdx.x, start, end, nb, S, cnt);
+}
+__global__ __launch_bounds__(TPB) void k_seg_counts(const uint32_t* __restrict__ off, uint32_t nb, uint32_t S2,
+                                                    uint32_t* __restrict__ cnt) {
+  msmk::seg_counts(blockIdx.x * TPB + threadIdx.x, off, nb, S2, cnt);
+}
+template <class F>
+__global__ __launch_bounds__(TPB) void k_accumulate(const uint32_t* __restrict__ points,
+                                                    const uint32_t* __restrict__ vals,
+                                                    const uint32_t* __restrict__ start,
+                                                    const uint32_t* __restrict__ end,
+                                                    const uint32_t* __restrict__ off, uint32_t nb, uint32_t S,
+                                                    uint32_t* __restrict__ out) {
+  msmk::accumulate<F>(blockIdx.x * TPB + threadIdx.x, points, vals, start, end, off, nb, S, out);
+}
+template <class F>
+__global__ __launch_bounds__(TPB) void k_merge(const uint32_t* __restrict__ in, const uint32_t* __restrict__ in_off,
+                                               const uint32_t* __restrict__ out_off, uint32_t nb, uint32_t S2,
+                                               uint32_t* __restrict__ out) {
+  msmk::merge<F>(blockIdx.x * TPB + threadIdx.x, in, in_off, out_off, nb, S2, out);
+}
+template <class F>
+__global__ __launch_bounds__(TPB) void k_merge_final(const uint32_t* __restrict__ in,
+                                                     const uint32_t* __restrict__ in_off, uint32_t nb,
+                                                     uint32_t* __restrict__ buckets) {
+  msmk::merge_final<F>(blockIdx.x * TPB + threadIdx.x, in, in_off, nb, buckets);
+}
+template <class F>
+__global__ __launch_bounds__(TPB) void k_reduce_first(const uint32_t* __restrict__ buckets, uint32_t nwin,
+                                                      uint32_t half, uint32_t L, uint32_t* __restrict__ s_out,
+                                                      uint32_t* __restrict__ t_out) {
+  msmk::reduce_first<F>(blockIdx.x * TPB + threadIdx.x, buckets, nwin, half, L, s_out, t_out);
+}
+template <class F>
+__global__ __launch_bounds__(TPB) void k_reduce_level(const uint32_t* __restrict__ s_in,
+                                                      const uint32_t* __restrict__ t_in, uint32_t nwin,
+                                                      uint32_t n_in, uint32_t L, int lg_width,
+                                                      uint32_t* __restrict__ s_out, uint32_t* __restrict__ t_out) {
+  msmk::reduce_level<F>(blockIdx.x * TPB + threadIdx.x, s_in, t_in, nwin, n_in, L, lg_width, s_out, t_out);
+}
+
+template <class F>
+void launch_accumulate(const uint32_t* points, const uint32_t* vals, const uint32_t* bstart, const uint32_t* bend,
+                       const uint32_t* off, uint32_t nb, uint32_t S, uint32_t* out, size_t max_tasks,
+                       hipStream_t st) {
+  hipLaunchKernelGGL(k_accumulate<F>, dim3(grid_for(max_tasks)), dim3(TPB), 0, st, points, vals, bstart, bend, off,
+                     nb, S, out);
+}
+
+}  // namespace
+
+MsmEngine::MsmEngine(Curve curve, size_t max_n, hipStream_t stream)
+    : curve_(curve), max_n_(std::max<size_t>(max_n, 1)), stream_(stream) {
+  if (max_n_ >= (size_t(1) << 31)) throw std::runtime_error("MSM size too large");
+  prm_ = MsmParams::for_size(max_n_);
+  fwords_ = curve == Curve::G1 ? 8 : 16;
+  const size_t half = size_t(1) << (prm_.c - 1);
+  nbuckets_ = (size_t)prm_.windows * half;
+  max_entries_ = max_n_ * prm_.windows;
+  if (max_entries_ >= 0xffffffffull) throw std::runtime_error("MSM size too large for 32-bit entry indices");
+  max_tasks_ = (max_entries_ + prm_.S - 1) / prm_.S + nbuckets_;
+  {
+    size_t m = (max_n_ + prm_.S - 1) / prm_.S;  // worst-case partials of one bucket
+    merge_levels_ = 0;
+    while (m > (size_t)prm_.S2) {
+      m = (m + prm_.S2 - 1) / prm_.S2;
+      ++merge_levels_;
+    }
+  }
+  const size_t xyzz_words = 4 * (size_t)fwords_;
+  HIPX(hipMalloc(&keys_, max_entries_ * 4));
+  HIPX(hipMalloc(&vals_, max_entries_ * 4));
+  HIPX(hipMalloc(&keys_sorted_, max_entries_ * 4));
+  HIPX(hipMalloc(&vals_sorted_, max_entries_ * 4));
+  HIPX(hipMalloc(&bstart_, (nbuckets_ + 1) * 4));
+  HIPX(hipMalloc(&bend_, (nbuckets_ + 1) * 4));
+  HIPX(hipMalloc(&cnt_, (nbuckets_ + 1) * 4));
+  HIPX(hipMalloc(&off_a_, (nbuckets_ + 1) * 4));
+  HIPX(hipMalloc(&off_b_, (nbuckets_ + 1) * 4));
+  HIPX(hipMalloc(&part_a_, max_tasks_ * xyzz_words * 4));
+  HIPX(hipMalloc(&part_b_, max_tasks_ * xyzz_words * 4));
+  HIPX(hipMalloc(&buckets_, nbuckets_ * xyzz_words * 4));
+  const size_t lvl1 = (size_t)prm_.windows * ((half + prm_.L - 1) / prm_.L);
+  for (int i = 0; i < 2; ++i) {
+    HIPX(hipMalloc(&lvl_s_[i], lvl1 * xyzz_words * 4));
+    HIPX(hipMalloc(&lvl_t_[i], lvl1 * xyzz_words * 4));
+  }
+  int end_bit = 1;
+  while ((size_t(1) << end_bit) <= nbuckets_) ++end_bit;
+  HIPX(hipcub::DeviceRadixSort::SortPairs(nullptr, sort_tmp_bytes_, keys_, keys_sorted_, vals_, vals_sorted_,
+                                          (int)max_entries_, 0, end_bit, stream_));
+  HIPX(hipMalloc(&sort_tmp_, sort_tmp_bytes_));
+  HIPX(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_tmp_bytes_, cnt_, off_a_, (int)(nbuckets_ + 1), stream_));
+  HIPX(hipMalloc(&scan_tmp_, scan_tmp_bytes_));
+}
+
+MsmEngine::~MsmEngine() {
+  for (void* p : {(void*)keys_, (void*)vals_, (void*)keys_sorted_, (void*)vals_sorted_, (void*)bstart_, (void*)bend_,
+                  (void*)cnt_, (void*)off_a_, (void*)off_b_, (void*)part_a_, (void*)part_b_, (void*)buckets_,
+                  (void*)lvl_s_[0], (void*)lvl_s_[1], (void*)lvl_t_[0], (void*)lvl_t_[1], sort_tmp_, scan_tmp_})
+    if (p) (void)hipFree(p);
+}
+
+void MsmEngine::run(const uint32_t* points, const uint32_t* scalars, size_t n, uint32_t* d_out) {
+  if (n > max_n_) throw std::runtime_error("MSM: n exceeds engine capacity");
+  const size_t xyzz_bytes = 16 * (size_t)fwords_;
+  const uint32_t W = (uint32_t)prm_.windows;
+  const uint32_t half = 1u << (prm_.c - 1);
+  const uint32_t nb = (uint32_t)nbuckets_;
+  hipStream_t st = stream_;
+  if (n == 0) {
+    // all windows = infinity
+    HIPX(hipMemsetAsync(buckets_, 0, nbuckets_ * xyzz_bytes, st));
+  } else {
+    const uint32_t total = (uint32_t)(n * W);
+    hipLaunchKernelGGL(k_digits, dim3(grid_for(n)), dim3(TPB), 0, st, scalars, (uint32_t)n, prm_.c, (int)W, keys_,
+                       vals_);
+    int end_bit = 1;
+    while ((size_t(1) << end_bit) <= nbuckets_) ++end_bit;
+    size_t tmp = sort_tmp_bytes_;
+    HIPX(hipcub::DeviceRadixSort::SortPairs(sort_tmp_, tmp, keys_, keys_sorted_, vals_, vals_sorted_, (int)total, 0,
+                                            end_bit, st));
+    HIPX(hipMemsetAsync(bstart_, 0, (nbuckets_ + 1) * 4, st));
+    HIPX(hipMemsetAsync(bend_, 0, (nbuckets_ + 1) * 4, st));
+    hipLaunchKernelGGL(k_bounds, dim3(grid_for(total)), dim3(TPB), 0, st, keys_sorted_, total, bstart_, bend_);
+    hipLaunchKernelGGL(k_task_counts, dim3(grid_for(nbuckets_ + 1)), dim3(TPB), 0, st, bstart_, bend_, nb,
+                       (uint32_t)prm_.S, cnt_);
+    size_t stmp = scan_tmp_bytes_;
+    HIPX(hipcub::DeviceScan::ExclusiveSum(scan_tmp_, stmp, cnt_, off_a_, (int)(nbuckets_ + 1), st));
+    const size_t max_tasks_now = ((size_t)total + prm_.S - 1) / prm_.S + nbuckets_;
+    if (curve_ == Curve::G1)
+      launch_accumulate<Fq>(points, vals_sorted_, bstart_, bend_, off_a_, nb, (uint32_t)prm_.S, part_a_,
+                            max_tasks_now, st);
+    else
+      launch_accumulate<Fq2>(points, vals_sorted_, bstart_, bend_, off_a_, nb, (uint32_t)prm_.S, part_a_,
+                             max_tasks_now, st);
+    // segmented merge levels: part_a/off_a -> part_b/off_b -> ...
+    uint32_t *pin = part_a_, *pout = part_b_, *oin = off_a_, *oout = off_b_;
+    size_t bound = max_tasks_now;
+    for (int lv = 0; lv < merge_levels_; ++lv) {
+      hipLaunchKernelGGL(k_seg_counts, dim3(grid_for(nbuckets_ + 1)), dim3(TPB), 0, st, oin, nb,
+                         (uint32_t)prm_.S2, cnt_);
+      stmp = scan_tmp_bytes_;
+      HIPX(hipcub::DeviceScan::ExclusiveSum(scan_tmp_, stmp, cnt_, oout, (int)(nbuckets_ + 1), st));
+      bound = (bound + prm_.S2 - 1) / prm_.S2 + nbuckets_;
+      if (curve_ == Curve::G1)
+        hipLaunchKernelGGL(k_merge<Fq>, dim3(grid_for(bound)), dim3(TPB), 0, st, pin, oin, oout, nb,
+                           (uint32_t)prm_.S2, pout);
+      else
+        hipLaunchKernelGGL(k_merge<Fq2>, dim3(grid_for(bound)), dim3(TPB), 0, st, pin, oin, oout, nb,
+                           (uint32_t)prm_.S2, pout);
+      std::swap(pin, pout);
+      std::swap(oin, oout);
+    }
+    if (curve_ == Curve::G1)
+      hipLaunchKernelGGL(k_merge_final<Fq>, dim3(grid_for(nbuckets_)), dim3(TPB), 0, st, pin, oin, nb, buckets_);
+    else
+      hipLaunchKernelGGL(k_merge_final<Fq2>, dim3(grid_for(nbuckets_)), dim3(TPB), 0, st, pin, oin, nb, buckets_);
+  }
+  // bucket reduction tree per window
+  const uint32_t L = (uint32_t)prm_.L;
+  uint32_t nodes = (half + L - 1) / L;
+  int cur = 0;
+  if (curve_ == Curve::G1)
+    hipLaunchKernelGGL(k_reduce_first<Fq>, dim3(grid_for((size_t)W * nodes)), dim3(TPB), 0, st, buckets_, W, half,
+                       L, lvl_s_[0], lvl_t_[0]);
+  else
+    hipLaunchKernelGGL(k_reduce_first<Fq2>, dim3(grid_for((size_t)W * nodes)), dim3(TPB), 0, st, buckets_, W, half,
+                       L, lvl_s_[0], lvl_t_[0]);
+  int lg_width = 0;
+  {
+    uint32_t l = L;
+    while (l > 1) {
+      l >>= 1;
+      ++lg_width;
+    }
+  }
+  const int lg_L = lg_width;
+  while (nodes > 1) {
+    const uint32_t next = (nodes + L - 1) / L;
+    if (curve_ == Curve::G1)
+      hipLaunchKernelGGL(k_reduce_level<Fq>, dim3(grid_for((size_t)W * next)), dim3(TPB), 0, st, lvl_s_[cur],
+                         lvl_t_[cur], W, nodes, L, lg_width, lvl_s_[cur ^ 1], lvl_t_[cur ^ 1]);
+    else
+      hipLaunchKernelGGL(k_reduce_level<Fq2>, dim3(grid_for((size_t)W * next)), dim3(TPB), 0, st, lvl_s_[cur],
+                         lvl_t_[cur], W, nodes, L, lg_width, lvl_s_[cur ^ 1], lvl_t_[cur ^ 1]);
+    cur ^= 1;
+    nodes = next;
+    lg_width += lg_L;
+  }
+  HIPX(hipGetLastError());
+  HIPX(hipMemcpyAsync(d_out, lvl_t_[cur], (size_t)W * xyzz_bytes, hipMemcpyDeviceToDevice, st));
+}
+
+}  // namespace zkp

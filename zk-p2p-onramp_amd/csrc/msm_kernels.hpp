@@ -1,0 +1,180 @@
+// Per-thread bodies of the MSM kernels (__host__ __device__ so that
+// tools/hosttest/msm_emu.cpp can replay the exact pipeline on the CPU).
+#pragma once
+#include "curve.hpp"
+
+namespace zkp {
+namespace msmk {
+
+ZDEV bool scalar_geq_r(const uint32_t (&s)[9]) {
+#pragma unroll
+  for (int i = 7; i >= 0; --i) {
+    if (s[i] != FrCfg::MOD_W[i]) return s[i] > FrCfg::MOD_W[i];
+  }
+  return true;
+}
+
+ZDEV void scalar_sub_r(uint32_t (&s)[9]) {
+  uint64_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    uint64_t d = (uint64_t)s[i] - FrCfg::MOD_W[i] - br;
+    s[i] = (uint32_t)d;
+    br = (d >> 63) & 1;
+  }
+}
+
+ZDEV void digits(uint32_t i, const uint32_t* __restrict__ scalars, uint32_t n, int c, int W,
+                uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+  if (i >= n) return;
+  const uint4* q = reinterpret_cast<const uint4*>(scalars + (size_t)i * 8);
+  uint4 a = q[0], b = q[1];
+  uint32_t s[9] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, 0u};
+  while (scalar_geq_r(s)) scalar_sub_r(s);  // snarkjs scalars are < r; others reduce (k*P == (k mod r)*P)
+  const uint32_t half = 1u << (c - 1), full = 1u << c, invalid = (uint32_t)W * half;
+  uint32_t carry = 0;
+  for (int w = 0; w < W; ++w) {
+    const int bit = w * c, j = bit >> 5, sh = bit & 31;
+    const uint64_t v = (uint64_t)s[j] | ((uint64_t)s[j + 1] << 32);
+    uint32_t raw = (uint32_t)(v >> sh) & (full - 1);
+    raw += carry;
+    uint32_t key, val = i;
+    if (raw > half) {
+      carry = 1;
+      const uint32_t mag = full - raw;  // digit = raw - 2^c <= 0 (0 when raw == 2^c: pure carry)
+      key = mag == 0 ? invalid : (uint32_t)w * half + mag - 1;
+      val |= 0x80000000u;
+    } else {
+      carry = 0;
+      key = raw == 0 ? invalid : (uint32_t)w * half + raw - 1;
+    }
+    keys[(size_t)w * n + i] = key;
+    vals[(size_t)w * n + i] = val;
+  }
+}
+
+ZDEV void bounds(uint32_t i, const uint32_t* __restrict__ keys, uint32_t total, uint32_t* __restrict__ start,
+                uint32_t* __restrict__ end) {
+  if (i >= total) return;
+  const uint32_t k = keys[i];
+  if (i == 0 || keys[i - 1] != k) start[k] = i;
+  if (i == total - 1 || keys[i + 1] != k) end[k] = i + 1;
+}
+
+// cnt[b] = ceil((end[b]-start[b]) / S) for b < nb, cnt[nb] = 0
+ZDEV void task_counts(uint32_t b, const uint32_t* __restrict__ start, const uint32_t* __restrict__ end, uint32_t nb,
+                     uint32_t S, uint32_t* __restrict__ cnt) {
+  if (b > nb) return;
+  cnt[b] = b == nb ? 0u : (end[b] - start[b] + S - 1) / S;
+}
+
+// cnt[b] = ceil((off[b+1]-off[b]) / S2) for b < nb, cnt[nb] = 0
+ZDEV void seg_counts(uint32_t b, const uint32_t* __restrict__ off, uint32_t nb, uint32_t S2,
+                    uint32_t* __restrict__ cnt) {
+  if (b > nb) return;
+  cnt[b] = b == nb ? 0u : (off[b + 1] - off[b] + S2 - 1) / S2;
+}
+
+// largest b in [0, nb) with off[b] <= t   (off[0] = 0 <= t < off[nb])
+ZDEV uint32_t seg_search(const uint32_t* __restrict__ off, uint32_t nb, uint32_t t) {
+  uint32_t lo = 0, hi = nb;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (off[mid] <= t)
+      lo = mid;
+    else
+      hi = mid;
+  }
+  return lo;
+}
+
+template <class F>
+ZDEV void accumulate(uint32_t t, const uint32_t* __restrict__ points, const uint32_t* __restrict__ vals,
+                     const uint32_t* __restrict__ start, const uint32_t* __restrict__ end,
+                     const uint32_t* __restrict__ off, uint32_t nb, uint32_t S, uint32_t* __restrict__ out) {
+  if (t >= off[nb]) return;
+  const uint32_t b = seg_search(off, nb, t);
+  const uint32_t s0 = start[b] + (t - off[b]) * S;
+  const uint32_t s1 = min(end[b], s0 + S);
+  Xyzz<F> acc = xyzz_inf<F>();
+  for (uint32_t j = s0; j < s1; ++j) {
+    const uint32_t v = vals[j];
+    Aff<F> p = load_aff<F>(points, v & 0x7fffffffu);
+    if (v >> 31) p.y = sub(f_zero<F>(), p.y);
+    xyzz_add_aff(acc, p);
+  }
+  store_xyzz(out, t, acc);
+}
+
+template <class F>
+ZDEV void merge(uint32_t t, const uint32_t* __restrict__ in, const uint32_t* __restrict__ in_off,
+                const uint32_t* __restrict__ out_off, uint32_t nb, uint32_t S2, uint32_t* __restrict__ out) {
+  if (t >= out_off[nb]) return;
+  const uint32_t b = seg_search(out_off, nb, t);
+  const uint32_t s0 = in_off[b] + (t - out_off[b]) * S2;
+  const uint32_t s1 = min(in_off[b + 1], s0 + S2);
+  Xyzz<F> acc = load_xyzz<F>(in, s0);
+  for (uint32_t j = s0 + 1; j < s1; ++j) xyzz_add(acc, load_xyzz<F>(in, j));
+  store_xyzz(out, t, acc);
+}
+
+// one thread per bucket: fold all its partials into buckets[b] (infinity if none)
+template <class F>
+ZDEV void merge_final(uint32_t b, const uint32_t* __restrict__ in, const uint32_t* __restrict__ in_off, uint32_t nb,
+                      uint32_t* __restrict__ buckets) {
+  if (b >= nb) return;
+  const uint32_t s0 = in_off[b], s1 = in_off[b + 1];
+  Xyzz<F> acc = xyzz_inf<F>();
+  for (uint32_t j = s0; j < s1; ++j) xyzz_add(acc, load_xyzz<F>(in, j));
+  store_xyzz(buckets, b, acc);
+}
+
+// level 1 of the bucket reduction: node g of window w covers buckets [gL, gL+L):
+//   S = sum B_k,  T = sum (j+1) B_(gL+j)
+template <class F>
+ZDEV void reduce_first(uint32_t id, const uint32_t* __restrict__ buckets, uint32_t nwin, uint32_t half, uint32_t L,
+                       uint32_t* __restrict__ s_out, uint32_t* __restrict__ t_out) {
+  const uint32_t nodes = (half + L - 1) / L;
+  if (id >= nwin * nodes) return;
+  const uint32_t w = id / nodes, g = id - w * nodes;
+  Xyzz<F> R = xyzz_inf<F>(), T = xyzz_inf<F>();
+  for (int j = (int)L - 1; j >= 0; --j) {
+    const uint32_t k = g * L + (uint32_t)j;
+    if (k < half) xyzz_add(R, load_xyzz<F>(buckets, (size_t)w * half + k));
+    xyzz_add(T, R);
+  }
+  store_xyzz(s_out, id, R);
+  store_xyzz(t_out, id, T);
+}
+
+// level l>1: node h of window w has children [hL, hL+L) of width 2^lg_width buckets:
+//   S' = sum S_j,  T' = sum T_j + 2^lg_width * sum j S_j
+template <class F>
+ZDEV void reduce_level(uint32_t id, const uint32_t* __restrict__ s_in, const uint32_t* __restrict__ t_in,
+                       uint32_t nwin, uint32_t n_in, uint32_t L, int lg_width, uint32_t* __restrict__ s_out,
+                       uint32_t* __restrict__ t_out) {
+  const uint32_t nodes = (n_in + L - 1) / L;
+  if (id >= nwin * nodes) return;
+  const uint32_t w = id / nodes, h = id - w * nodes;
+  Xyzz<F> R = xyzz_inf<F>(), U = xyzz_inf<F>(), Tsum = xyzz_inf<F>();
+  for (int j = (int)L - 1; j >= 1; --j) {
+    const uint32_t k = h * L + (uint32_t)j;
+    if (k < n_in) {
+      xyzz_add(R, load_xyzz<F>(s_in, (size_t)w * n_in + k));
+      xyzz_add(Tsum, load_xyzz<F>(t_in, (size_t)w * n_in + k));
+    }
+    xyzz_add(U, R);
+  }
+  {
+    const uint32_t k = h * L;
+    xyzz_add(R, load_xyzz<F>(s_in, (size_t)w * n_in + k));
+    xyzz_add(Tsum, load_xyzz<F>(t_in, (size_t)w * n_in + k));
+  }
+  for (int i = 0; i < lg_width; ++i) U = xyzz_dbl(U);
+  xyzz_add(Tsum, U);
+  store_xyzz(s_out, id, R);
+  store_xyzz(t_out, id, Tsum);
+}
+
+}  // namespace msmk
+}  // namespace zkp

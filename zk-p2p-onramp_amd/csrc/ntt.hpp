@@ -1,0 +1,58 @@
+// Fr NTT engine for the QAP quotient on gfx950.
+//
+// Replaces ffjavascript Fr.ifft / Fr.batchApplyKey / Fr.fft as used by snarkjs
+// groth16_prove: for each of A, B, C
+//   evaluations on <w> (natural order)  --iNTT-->  coefficients
+//   --x g^i-->  --NTT-->  evaluations on the coset g<w> (natural order)
+// with w = Fr.w[log2 n] and g = Fr.w[log2 n + 1] (ffjavascript convention).
+//
+// Multi-pass "four-step" structure: a pass splits the current block of size m
+// into n1 x n2, runs n1-point DFTs in LDS over the strided j1 index for a tile
+// of consecutive columns (radix-2 stages, LDS-resident), and multiplies by the
+// inter-pass twiddle w_m^(j2*k1).  The inverse runs these passes DIF-style
+// (natural in -> digit-reversed out); the forward runs the TRANSPOSED passes in
+// reverse order (digit-reversed in -> natural out), so no permutation pass is
+// ever needed; the coset key g^i / n is applied in digit-reversed index space.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <vector>
+
+namespace zkp {
+
+class NttEngine {
+ public:
+  NttEngine(int log_n, hipStream_t stream);
+  ~NttEngine();
+  NttEngine(const NttEngine&) = delete;
+  NttEngine& operator=(const NttEngine&) = delete;
+
+  int log_n() const { return log_n_; }
+  // data: n Fr elements, device layout (Montgomery R' = 2^261, 8 LE words each)
+  // natural-order evaluations on <w>  ->  natural-order evaluations on g<w>
+  void coset_extend(uint32_t* data);
+  // plain transforms (natural in, natural out), for tests
+  void forward(uint32_t* data);  // A_j = sum a_i w^(ij)
+  void inverse(uint32_t* data);  // a_i = n^-1 sum A_j w^(-ij)
+  hipStream_t stream() const { return stream_; }
+
+ private:
+  void dif_passes(uint32_t* data, bool inverse_root);
+  void dit_passes(uint32_t* data, bool inverse_root);
+  void scale(uint32_t* data, int mode);  // 0: x g^f(pos)/n   1: x 1/n (digit-reversed layout ok)
+  void digit_reverse(uint32_t* data, bool to_natural);
+  int log_n_;
+  hipStream_t stream_;
+  std::vector<int> bits_;  // pass radix bits (DIF order)
+  int h_ = 0;              // split of the twiddle exponent tables
+  // device tables (dev layout): [0] forward root, [1] inverse root
+  uint32_t* tw_lo_[2] = {nullptr, nullptr};
+  uint32_t* tw_hi_[2] = {nullptr, nullptr};
+  uint32_t* loc_[2] = {nullptr, nullptr};  // local roots w_(2^b)^e, for every b <= 10, e < 2^(b-1): packed by b
+  uint32_t* coset_lo_ = nullptr;           // g^e / n, e < 2^h
+  uint32_t* coset_hi_ = nullptr;           // g^(e 2^h)
+  uint32_t* ninv_ = nullptr;               // 1/n (dev form)
+  uint32_t* scratch_ = nullptr;            // for digit_reverse (tests only)
+};
+
+}  // namespace zkp

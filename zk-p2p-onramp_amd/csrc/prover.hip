@@ -1,0 +1,585 @@
+// Groth16 prover core (see prover.hpp).
+#include "prover.hpp"
+
+#include <sys/random.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <exception>
+#include <thread>
+
+#include "hip_check.hpp"
+#include "qap.hpp"
+
+namespace zkp {
+
+using host::Affine;
+using host::Jac;
+using host::U256;
+using HFq = host::Fq;
+using HFq2 = host::Fq2;
+using HFr = host::Fr;
+
+// ------------------------------------------------------------------ parsing
+
+BinFile parse_binfile(const uint8_t* buf, size_t len, const char* magic, uint32_t max_version) {
+  if (!buf || len < 12 || std::memcmp(buf, magic, 4) != 0)
+    throw ZkpError(ZKP_ERR_FORMAT, std::string(magic) + ": Invalid File format");
+  BinFile bf;
+  uint32_t nsec;
+  std::memcpy(&bf.version, buf + 4, 4);
+  std::memcpy(&nsec, buf + 8, 4);
+  if (bf.version > max_version) throw ZkpError(ZKP_ERR_FORMAT, std::string(magic) + ": Version not supported");
+  size_t pos = 12;
+  for (uint32_t i = 0; i < nsec; ++i) {
+    if (pos + 12 > len) throw ZkpError(ZKP_ERR_FORMAT, std::string(magic) + ": truncated section header");
+    uint32_t id;
+    uint64_t sl;
+    std::memcpy(&id, buf + pos, 4);
+    std::memcpy(&sl, buf + pos + 4, 8);
+    pos += 12;
+    if (sl > len - pos) throw ZkpError(ZKP_ERR_FORMAT, std::string(magic) + ": truncated section " + std::to_string(id));
+    if (id < 16 && !bf.sec[id].ptr) bf.sec[id] = Section{buf + pos, sl};
+    pos += sl;
+  }
+  return bf;
+}
+
+static uint32_t rd32(const uint8_t* p) {
+  uint32_t v;
+  std::memcpy(&v, p, 4);
+  return v;
+}
+
+static const uint8_t R_LE[32] = {0x01, 0x00, 0x00, 0xf0, 0x93, 0xf5, 0xe1, 0x43, 0x91, 0x70, 0xb9, 0x79, 0x48, 0xe8, 0x33, 0x28,
+                                 0x5d, 0x58, 0x81, 0x81, 0xb6, 0x45, 0x50, 0xb8, 0x29, 0xa0, 0x31, 0xe1, 0x72, 0x4e, 0x64, 0x30};
+static const uint8_t P_LE[32] = {0x47, 0xfd, 0x7c, 0xd8, 0x16, 0x8c, 0x20, 0x3c, 0x8d, 0xca, 0x71, 0x68, 0x91, 0x6a, 0x81, 0x97,
+                                 0x5d, 0x58, 0x81, 0x81, 0xb6, 0x45, 0x50, 0xb8, 0x29, 0xa0, 0x31, 0xe1, 0x72, 0x4e, 0x64, 0x30};
+
+WtnsView parse_wtns(const uint8_t* buf, size_t len) {
+  BinFile bf = parse_binfile(buf, len, "wtns", 2);
+  const Section& s1 = bf.sec[1];
+  const Section& s2 = bf.sec[2];
+  if (!s1.ptr || !s2.ptr || s1.len < 4) throw ZkpError(ZKP_ERR_FORMAT, "wtns: missing header or witness section");
+  const uint32_t n8 = rd32(s1.ptr);
+  if (s1.len < 8 + (uint64_t)n8) throw ZkpError(ZKP_ERR_FORMAT, "wtns: bad header section");
+  if (n8 != 32 || std::memcmp(s1.ptr + 4, R_LE, 32) != 0)
+    throw ZkpError(ZKP_ERR_CURVE, "Curve of the witness does not match the curve of the proving key");
+  WtnsView v;
+  v.n_witness = rd32(s1.ptr + 4 + n8);
+  if (s2.len != (uint64_t)v.n_witness * 32) throw ZkpError(ZKP_ERR_FORMAT, "wtns: Invalid witness section size");
+  v.values = s2.ptr;
+  return v;
+}
+
+static HFq fq_from_zkey(const uint8_t* p) {
+  U256 v = host::u256_from_le(p);
+  if (host::u256_geq(v, host::FQ_DESC.mod)) throw ZkpError(ZKP_ERR_FORMAT, "zkey: point coordinate out of range");
+  return HFq::raw(v);  // zkey stores Montgomery(2^256) = host representation
+}
+
+static Affine<HFq> g1_from_zkey(const uint8_t* p) {
+  Affine<HFq> a{fq_from_zkey(p), fq_from_zkey(p + 32), false};
+  a.inf = a.x.is_zero() && a.y.is_zero();
+  return a;
+}
+
+static Affine<HFq2> g2_from_zkey(const uint8_t* p) {
+  Affine<HFq2> a{HFq2{fq_from_zkey(p), fq_from_zkey(p + 32)}, HFq2{fq_from_zkey(p + 64), fq_from_zkey(p + 96)}, false};
+  a.inf = a.x.is_zero() && a.y.is_zero();
+  return a;
+}
+
+struct Csr {
+  std::vector<uint32_t> rowptr, col, val;  // val: 8 words per entry (raw zkey bytes)
+};
+
+struct ZkeyParsed {
+  BinFile bf;
+  ZkeyHeader hdr;
+  Csr csr[2];
+};
+
+static ZkeyParsed parse_zkey(const uint8_t* buf, size_t len) {
+  ZkeyParsed z;
+  z.bf = parse_binfile(buf, len, "zkey", 1);
+  const Section& s1 = z.bf.sec[1];
+  if (!s1.ptr || s1.len < 4) throw ZkpError(ZKP_ERR_FORMAT, "zkey: missing header section");
+  if (rd32(s1.ptr) != 1) throw ZkpError(ZKP_ERR_PROTOCOL, "zkey file is not groth16");
+  const Section& s2 = z.bf.sec[2];
+  if (!s2.ptr) throw ZkpError(ZKP_ERR_FORMAT, "zkey: missing groth16 header section");
+  const uint8_t* p = s2.ptr;
+  const uint8_t* end = s2.ptr + s2.len;
+  auto need = [&](size_t n) {
+    if ((size_t)(end - p) < n) throw ZkpError(ZKP_ERR_FORMAT, "zkey: truncated groth16 header");
+  };
+  need(4);
+  uint32_t n8q = rd32(p);
+  p += 4;
+  need(n8q + 4);
+  if (n8q != 32 || std::memcmp(p, P_LE, 32) != 0) throw ZkpError(ZKP_ERR_CURVE, "zkey: curve not supported (need bn128)");
+  p += n8q;
+  uint32_t n8r = rd32(p);
+  p += 4;
+  need(n8r + 12);
+  if (n8r != 32 || std::memcmp(p, R_LE, 32) != 0) throw ZkpError(ZKP_ERR_CURVE, "zkey: curve not supported (need bn128)");
+  p += n8r;
+  ZkeyHeader& h = z.hdr;
+  h.n_vars = rd32(p);
+  h.n_public = rd32(p + 4);
+  h.domain_size = rd32(p + 8);
+  p += 12;
+  need(64 * 3 + 128 * 3);
+  h.alpha1 = g1_from_zkey(p);
+  h.beta1 = g1_from_zkey(p + 64);
+  h.beta2 = g2_from_zkey(p + 128);
+  h.gamma2 = g2_from_zkey(p + 256);
+  h.delta1 = g1_from_zkey(p + 384);
+  h.delta2 = g2_from_zkey(p + 448);
+  if (h.domain_size == 0 || (h.domain_size & (h.domain_size - 1)))
+    throw ZkpError(ZKP_ERR_FORMAT, "zkey: domain size is not a power of two");
+  while ((1u << h.log_domain) < h.domain_size) ++h.log_domain;
+  if (h.log_domain > 27) throw ZkpError(ZKP_ERR_FORMAT, "zkey: domain larger than 2^27 not supported");
+  if (h.n_vars < h.n_public + 1) throw ZkpError(ZKP_ERR_FORMAT, "zkey: nVars < nPublic + 1");
+  auto chk = [&](int id, uint64_t want) {
+    if (!z.bf.sec[id].ptr || z.bf.sec[id].len != want)
+      throw ZkpError(ZKP_ERR_FORMAT, "zkey: section " + std::to_string(id) + " has an invalid size");
+  };
+  chk(5, (uint64_t)h.n_vars * 64);
+  chk(6, (uint64_t)h.n_vars * 64);
+  chk(7, (uint64_t)h.n_vars * 128);
+  chk(8, (uint64_t)(h.n_vars - h.n_public - 1) * 64);
+  chk(9, (uint64_t)h.domain_size * 64);
+  const Section& s4 = z.bf.sec[4];
+  if (!s4.ptr || s4.len < 4) throw ZkpError(ZKP_ERR_FORMAT, "zkey: missing coefficients section");
+  h.n_coef = rd32(s4.ptr);
+  if (s4.len != 4 + (uint64_t)h.n_coef * 44) throw ZkpError(ZKP_ERR_FORMAT, "zkey: coefficients section has an invalid size");
+  // CSR by (matrix, constraint) with a stable counting sort
+  for (int m = 0; m < 2; ++m) z.csr[m].rowptr.assign((size_t)h.domain_size + 1, 0);
+  const uint8_t* c = s4.ptr + 4;
+  for (uint32_t i = 0; i < h.n_coef; ++i, c += 44) {
+    const uint32_t m = rd32(c), row = rd32(c + 4), sig = rd32(c + 8);
+    if (m > 1 || row >= h.domain_size || sig >= h.n_vars)
+      throw ZkpError(ZKP_ERR_FORMAT, "zkey: coefficient entry out of range");
+    z.csr[m].rowptr[row + 1]++;
+  }
+  for (int m = 0; m < 2; ++m) {
+    auto& rp = z.csr[m].rowptr;
+    for (size_t r = 0; r < h.domain_size; ++r) rp[r + 1] += rp[r];
+    z.csr[m].col.resize(rp.back());
+    z.csr[m].val.resize((size_t)rp.back() * 8);
+  }
+  std::vector<uint32_t> fill[2] = {std::vector<uint32_t>(z.csr[0].rowptr.begin(), z.csr[0].rowptr.end() - 1),
+                                   std::vector<uint32_t>(z.csr[1].rowptr.begin(), z.csr[1].rowptr.end() - 1)};
+  c = s4.ptr + 4;
+  for (uint32_t i = 0; i < h.n_coef; ++i, c += 44) {
+    const uint32_t m = rd32(c), row = rd32(c + 4), sig = rd32(c + 8);
+    const uint32_t at = fill[m][row]++;
+    z.csr[m].col[at] = sig;
+    std::memcpy(&z.csr[m].val[(size_t)at * 8], c + 12, 32);
+  }
+  return z;
+}
+
+// ------------------------------------------------------------------ host EC helpers
+
+static HFq2 fq2_from_dev(const uint32_t* w) { return HFq2{host::fq_from_dev(w), host::fq_from_dev(w + 8)}; }
+
+template <class F>
+static F f_from_dev(const uint32_t* w);
+template <>
+HFq f_from_dev<HFq>(const uint32_t* w) {
+  return host::fq_from_dev(w);
+}
+template <>
+HFq2 f_from_dev<HFq2>(const uint32_t* w) {
+  return fq2_from_dev(w);
+}
+
+// fold W window sums (XYZZ device layout) by Horner: sum_w 2^(c w) T_w
+template <class F>
+static Jac<F> fold_windows(const uint32_t* win, int W, int c) {
+  constexpr int FW = sizeof(F) == sizeof(HFq) ? 8 : 16;
+  auto load = [&](int w) {
+    const uint32_t* p = win + (size_t)w * 4 * FW;
+    return host::jac_from_xyzz(f_from_dev<F>(p), f_from_dev<F>(p + FW), f_from_dev<F>(p + 2 * FW),
+                               f_from_dev<F>(p + 3 * FW));
+  };
+  Jac<F> acc = load(W - 1);
+  for (int w = W - 2; w >= 0; --w) {
+    for (int i = 0; i < c; ++i) acc = host::jac_dbl(acc);
+    acc = host::jac_add(acc, load(w));
+  }
+  return acc;
+}
+
+static U256 scalar_or_random(const uint8_t* s32) {
+  U256 v;
+  if (s32) {
+    v = host::u256_from_le(s32);
+    while (host::u256_geq(v, host::FR_DESC.mod)) host::u256_sub(v, host::FR_DESC.mod);
+    return v;
+  }
+  for (;;) {
+    uint8_t b[32];
+    size_t got = 0;
+    while (got < 32) {
+      ssize_t k = getrandom(b + got, 32 - got, 0);
+      if (k <= 0) throw ZkpError(ZKP_ERR_INTERNAL, "getrandom failed");
+      got += (size_t)k;
+    }
+    b[31] &= 0x3f;  // 254 bits
+    v = host::u256_from_le(b);
+    if (!host::u256_geq(v, host::FR_DESC.mod)) return v;
+  }
+}
+
+static void put_fq(const HFq& x, uint8_t* out) { host::u256_to_le(x.to_std(), out); }
+
+// ------------------------------------------------------------------ device pipeline
+
+class DevicePipeline {
+ public:
+  DevicePipeline(int dev, const ZkeyParsed& z) : dev_(dev), hdr_(z.hdr) {
+    HIPX(hipSetDevice(dev_));
+    HIPX(hipStreamCreateWithFlags(&s0_, hipStreamNonBlocking));
+    HIPX(hipStreamCreateWithFlags(&s1_, hipStreamNonBlocking));
+    for (auto& e : ev_) HIPX(hipEventCreate(&e));
+    const ZkeyHeader& h = hdr_;
+    const size_t nv = h.n_vars, nd = h.domain_size, nc = h.n_vars - h.n_public - 1;
+    auto up = [&](const Section& s, size_t bytes) {
+      uint32_t* d = nullptr;
+      HIPX(hipMalloc(&d, std::max<size_t>(bytes, 64)));
+      if (bytes) HIPX(hipMemcpyAsync(d, s.ptr, bytes, hipMemcpyHostToDevice, s0_));
+      return d;
+    };
+    pa_ = up(z.bf.sec[5], nv * 64);
+    pb1_ = up(z.bf.sec[6], nv * 64);
+    pb2_ = up(z.bf.sec[7], nv * 128);
+    pc_ = up(z.bf.sec[8], nc * 64);
+    ph_ = up(z.bf.sec[9], nd * 64);
+    launch_convert_fq_zkey(pa_, nv * 2, s0_);
+    launch_convert_fq_zkey(pb1_, nv * 2, s0_);
+    launch_convert_fq_zkey(pb2_, nv * 4, s0_);
+    launch_convert_fq_zkey(pc_, nc * 2, s0_);
+    launch_convert_fq_zkey(ph_, nd * 2, s0_);
+    for (int m = 0; m < 2; ++m) {
+      const Csr& c = z.csr[m];
+      HIPX(hipMalloc(&rowptr_[m], c.rowptr.size() * 4));
+      HIPX(hipMemcpyAsync(rowptr_[m], c.rowptr.data(), c.rowptr.size() * 4, hipMemcpyHostToDevice, s0_));
+      HIPX(hipMalloc(&col_[m], std::max<size_t>(c.col.size() * 4, 4)));
+      HIPX(hipMalloc(&val_[m], std::max<size_t>(c.val.size() * 4, 32)));
+      if (!c.col.empty()) {
+        HIPX(hipMemcpyAsync(col_[m], c.col.data(), c.col.size() * 4, hipMemcpyHostToDevice, s0_));
+        HIPX(hipMemcpyAsync(val_[m], c.val.data(), c.val.size() * 4, hipMemcpyHostToDevice, s0_));
+        launch_convert_coefs(val_[m], c.col.size(), s0_);
+      }
+    }
+    HIPX(hipMalloc(&wit_, std::max<size_t>(nv * 32, 32)));
+    for (auto& b : abc_) HIPX(hipMalloc(&b, nd * 32));
+    HIPX(hipMalloc(&pscal_, nd * 32));
+    ntt_ = std::make_unique<NttEngine>((int)h.log_domain, s0_);
+    g1_ = std::make_unique<MsmEngine>(Curve::G1, std::max<size_t>(nv, nd), s0_);
+    g2_ = std::make_unique<MsmEngine>(Curve::G2, nv, s1_);
+    win1_ = g1_->window_words();
+    win2_ = g2_->window_words();
+    HIPX(hipMalloc(&dwin_, (4 * win1_ + win2_) * 4));
+    HIPX(hipHostMalloc(&hwin_, (4 * win1_ + win2_) * 4, hipHostMallocDefault));
+    HIPX(hipStreamSynchronize(s0_));
+  }
+
+  ~DevicePipeline() {
+    (void)hipSetDevice(dev_);
+    ntt_.reset();
+    g1_.reset();
+    g2_.reset();
+    for (void* p : {(void*)pa_, (void*)pb1_, (void*)pb2_, (void*)pc_, (void*)ph_, (void*)rowptr_[0], (void*)rowptr_[1],
+                    (void*)col_[0], (void*)col_[1], (void*)val_[0], (void*)val_[1], (void*)wit_, (void*)abc_[0],
+                    (void*)abc_[1], (void*)abc_[2], (void*)pscal_, (void*)dwin_})
+      if (p) (void)hipFree(p);
+    if (hwin_) (void)hipHostFree(hwin_);
+    for (auto& e : ev_) (void)hipEventDestroy(e);
+    (void)hipStreamDestroy(s0_);
+    (void)hipStreamDestroy(s1_);
+  }
+
+  // enqueue witness upload + quotient (A4..A8); result scalars in pscal_
+  void enqueue_quotient(const WtnsView& w) {
+    const ZkeyHeader& h = hdr_;
+    HIPX(hipEventRecord(ev_[0], s0_));
+    HIPX(hipMemcpyAsync(wit_, w.values, (size_t)h.n_vars * 32, hipMemcpyHostToDevice, s0_));
+    HIPX(hipEventRecord(ev_[1], s0_));
+    launch_build_abc(rowptr_[0], col_[0], val_[0], rowptr_[1], col_[1], val_[1], wit_, h.domain_size, abc_[0],
+                     abc_[1], abc_[2], s0_);
+    HIPX(hipEventRecord(ev_[2], s0_));
+    for (auto* b : abc_) ntt_->coset_extend(b);
+    launch_join_abc(abc_[0], abc_[1], abc_[2], h.domain_size, pscal_, s0_);
+    HIPX(hipEventRecord(ev_[3], s0_));
+  }
+
+  void quotient(const WtnsView& w, uint8_t* out) {
+    std::lock_guard<std::mutex> lk(mu_);
+    HIPX(hipSetDevice(dev_));
+    enqueue_quotient(w);
+    HIPX(hipMemcpyAsync(out, pscal_, (size_t)hdr_.domain_size * 32, hipMemcpyDeviceToHost, s0_));
+    HIPX(hipStreamSynchronize(s0_));
+  }
+
+  struct MsmOut {
+    Jac<HFq> a, b1, c, h;
+    Jac<HFq2> b2;
+    float ms[5];
+  };
+
+  MsmOut prove(const WtnsView& w) {
+    std::lock_guard<std::mutex> lk(mu_);
+    HIPX(hipSetDevice(dev_));
+    const ZkeyHeader& h = hdr_;
+    enqueue_quotient(w);
+    // G2 MSM (B2) on s1 as soon as the witness is resident
+    HIPX(hipStreamWaitEvent(s1_, ev_[1], 0));
+    HIPX(hipEventRecord(ev_[7], s1_));
+    g2_->run(pb2_, wit_, h.n_vars, dwin_ + 4 * win1_);
+    HIPX(hipEventRecord(ev_[6], s1_));
+    // G1 MSMs on s0 after the quotient
+    g1_->run(pa_, wit_, h.n_vars, dwin_);
+    g1_->run(pb1_, wit_, h.n_vars, dwin_ + win1_);
+    g1_->run(pc_, wit_ + (size_t)(h.n_public + 1) * 8, h.n_vars - h.n_public - 1, dwin_ + 2 * win1_);
+    g1_->run(ph_, pscal_, h.domain_size, dwin_ + 3 * win1_);
+    HIPX(hipEventRecord(ev_[4], s0_));
+    HIPX(hipStreamWaitEvent(s0_, ev_[6], 0));
+    HIPX(hipMemcpyAsync(hwin_, dwin_, (4 * win1_ + win2_) * 4, hipMemcpyDeviceToHost, s0_));
+    HIPX(hipEventRecord(ev_[5], s0_));
+    HIPX(hipStreamSynchronize(s0_));
+    MsmOut o;
+    const int W1 = g1_->params().windows, c1 = g1_->params().c;
+    const int W2 = g2_->params().windows, c2 = g2_->params().c;
+    o.a = fold_windows<HFq>(hwin_, W1, c1);
+    o.b1 = fold_windows<HFq>(hwin_ + win1_, W1, c1);
+    o.c = fold_windows<HFq>(hwin_ + 2 * win1_, W1, c1);
+    o.h = fold_windows<HFq>(hwin_ + 3 * win1_, W1, c1);
+    o.b2 = fold_windows<HFq2>(hwin_ + 4 * win1_, W2, c2);
+    HIPX(hipEventElapsedTime(&o.ms[0], ev_[0], ev_[1]));  // wtns H2D
+    HIPX(hipEventElapsedTime(&o.ms[1], ev_[1], ev_[2]));  // buildABC
+    HIPX(hipEventElapsedTime(&o.ms[2], ev_[2], ev_[3]));  // NTT + join
+    HIPX(hipEventElapsedTime(&o.ms[3], ev_[3], ev_[4]));  // G1 MSMs
+    HIPX(hipEventElapsedTime(&o.ms[4], ev_[7], ev_[6]));  // G2 MSM
+    return o;
+  }
+
+ private:
+  int dev_;
+  ZkeyHeader hdr_;
+  hipStream_t s0_ = nullptr, s1_ = nullptr;
+  hipEvent_t ev_[8];
+  uint32_t *pa_ = nullptr, *pb1_ = nullptr, *pb2_ = nullptr, *pc_ = nullptr, *ph_ = nullptr;
+  uint32_t* rowptr_[2] = {nullptr, nullptr};
+  uint32_t* col_[2] = {nullptr, nullptr};
+  uint32_t* val_[2] = {nullptr, nullptr};
+  uint32_t* wit_ = nullptr;
+  uint32_t* abc_[3] = {nullptr, nullptr, nullptr};
+  uint32_t* pscal_ = nullptr;
+  std::unique_ptr<NttEngine> ntt_;
+  std::unique_ptr<MsmEngine> g1_, g2_;
+  size_t win1_ = 0, win2_ = 0;
+  uint32_t* dwin_ = nullptr;
+  uint32_t* hwin_ = nullptr;
+  std::mutex mu_;
+};
+
+// ------------------------------------------------------------------ Prover
+
+Prover::Prover(const uint8_t* zkey, size_t len, const std::vector<int>& devices) {
+  ZkeyParsed z = parse_zkey(zkey, len);
+  hdr_ = z.hdr;
+  int ndev = 0;
+  HIPX(hipGetDeviceCount(&ndev));
+  if (ndev <= 0) throw ZkpError(ZKP_ERR_DEVICE, "no HIP device available");
+  std::vector<int> devs = devices.empty() ? std::vector<int>{0} : devices;
+  for (int d : devs) {
+    if (d < 0 || d >= ndev) throw ZkpError(ZKP_ERR_INVALID_ARG, "device ordinal out of range");
+    devs_.push_back(std::make_unique<DevicePipeline>(d, z));
+  }
+}
+
+Prover::~Prover() = default;
+
+static void assemble(const ZkeyHeader& h, const DevicePipeline::MsmOut& m, const WtnsView& w, const uint8_t* r32,
+                     const uint8_t* s32, zkp_proof* out) {
+  const U256 r = scalar_or_random(r32), s = scalar_or_random(s32);
+  const Jac<HFq> alpha1 = host::jac_from_aff(h.alpha1), beta1 = host::jac_from_aff(h.beta1),
+                 delta1 = host::jac_from_aff(h.delta1);
+  const Jac<HFq2> beta2 = host::jac_from_aff(h.beta2), delta2 = host::jac_from_aff(h.delta2);
+  // A = piA' + alpha1 + r delta1
+  Jac<HFq> A = host::jac_add(host::jac_add(m.a, alpha1), host::jac_mul(delta1, r));
+  // B = piB' + beta2 + s delta2 ; B1 = piB1' + beta1 + s delta1
+  Jac<HFq2> B = host::jac_add(host::jac_add(m.b2, beta2), host::jac_mul(delta2, s));
+  Jac<HFq> B1 = host::jac_add(host::jac_add(m.b1, beta1), host::jac_mul(delta1, s));
+  // C = piC' + piH + s A + r B1 - (r s) delta1
+  HFr rs = HFr::from_std(r) * HFr::from_std(s);
+  U256 nrs = rs.neg().to_std();
+  Jac<HFq> C = host::jac_add(m.c, m.h);
+  C = host::jac_add(C, host::jac_mul(A, s));
+  C = host::jac_add(C, host::jac_mul(B1, r));
+  C = host::jac_add(C, host::jac_mul(delta1, nrs));
+  auto a = host::jac_to_aff(A);
+  auto b = host::jac_to_aff(B);
+  auto c = host::jac_to_aff(C);
+  put_fq(a.x, out->pi_a[0]);
+  put_fq(a.y, out->pi_a[1]);
+  put_fq(b.x.c0, out->pi_b[0][0]);
+  put_fq(b.x.c1, out->pi_b[0][1]);
+  put_fq(b.y.c0, out->pi_b[1][0]);
+  put_fq(b.y.c1, out->pi_b[1][1]);
+  put_fq(c.x, out->pi_c[0]);
+  put_fq(c.y, out->pi_c[1]);
+  out->n_public = h.n_public;
+  if (out->public_signals && out->public_capacity)
+    std::memcpy(out->public_signals, w.values + 32, (size_t)std::min(h.n_public, out->public_capacity) * 32);
+}
+
+static WtnsView check_wtns(const ZkeyHeader& h, const uint8_t* wtns, size_t len) {
+  WtnsView w = parse_wtns(wtns, len);
+  if (w.n_witness != h.n_vars)
+    throw ZkpError(ZKP_ERR_WITNESS_LENGTH, "Invalid witness length. Circuit: " + std::to_string(h.n_vars) +
+                                               ", witness: " + std::to_string(w.n_witness));
+  return w;
+}
+
+void Prover::prove(const uint8_t* wtns, size_t len, const uint8_t* r32, const uint8_t* s32, zkp_proof* out) {
+  auto t0 = std::chrono::steady_clock::now();
+  WtnsView w = check_wtns(hdr_, wtns, len);
+  DevicePipeline& d = *devs_[rr_.fetch_add(1) % devs_.size()];
+  DevicePipeline::MsmOut m = d.prove(w);
+  auto t1 = std::chrono::steady_clock::now();
+  assemble(hdr_, m, w, r32, s32, out);
+  auto t2 = std::chrono::steady_clock::now();
+  std::lock_guard<std::mutex> lk(tmu_);
+  for (int i = 0; i < 5; ++i) last_ms_[i] = m.ms[i];
+  last_ms_[5] = std::chrono::duration<float, std::milli>(t2 - t1).count();
+  last_ms_[6] = std::chrono::duration<float, std::milli>(t2 - t0).count();
+}
+
+void Prover::prove_batch(const uint8_t* const* wtns, const size_t* lens, int n, const uint8_t* const* r32s,
+                         const uint8_t* const* s32s, zkp_proof* outs) {
+  std::atomic<int> next{0};
+  std::vector<std::exception_ptr> errs(devs_.size());
+  std::vector<std::thread> th;
+  for (size_t di = 0; di < devs_.size(); ++di) {
+    th.emplace_back([&, di] {
+      try {
+        for (;;) {
+          const int i = next.fetch_add(1);
+          if (i >= n) break;
+          WtnsView w = check_wtns(hdr_, wtns[i], lens[i]);
+          DevicePipeline::MsmOut m = devs_[di]->prove(w);
+          assemble(hdr_, m, w, r32s ? r32s[i] : nullptr, s32s ? s32s[i] : nullptr, &outs[i]);
+        }
+      } catch (...) {
+        errs[di] = std::current_exception();
+        next.store(n);
+      }
+    });
+  }
+  for (auto& t : th) t.join();
+  for (auto& e : errs)
+    if (e) std::rethrow_exception(e);
+}
+
+void Prover::quotient(const uint8_t* wtns, size_t len, uint8_t* out) {
+  WtnsView w = check_wtns(hdr_, wtns, len);
+  devs_[0]->quotient(w, out);
+}
+
+void Prover::timings(float* ms, int n) const {
+  std::lock_guard<std::mutex> lk(tmu_);
+  for (int i = 0; i < n && i < 7; ++i) ms[i] = last_ms_[i];
+}
+
+// ------------------------------------------------------------------ kernel-level helpers
+
+void msm_points(int device, Curve curve, const uint8_t* points, const uint8_t* scalars, size_t n, uint8_t* out,
+                int* is_inf) {
+  HIPX(hipSetDevice(device));
+  hipStream_t st;
+  HIPX(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  const size_t pbytes = n * (curve == Curve::G1 ? 64 : 128);
+  uint32_t *dp = nullptr, *ds = nullptr, *dw = nullptr;
+  try {
+    MsmEngine eng(curve, std::max<size_t>(n, 1), st);
+    HIPX(hipMalloc(&dp, std::max<size_t>(pbytes, 64)));
+    HIPX(hipMalloc(&ds, std::max<size_t>(n * 32, 32)));
+    HIPX(hipMalloc(&dw, eng.window_words() * 4));
+    if (n) {
+      HIPX(hipMemcpyAsync(dp, points, pbytes, hipMemcpyHostToDevice, st));
+      HIPX(hipMemcpyAsync(ds, scalars, n * 32, hipMemcpyHostToDevice, st));
+      launch_convert_fq_zkey(dp, n * (curve == Curve::G1 ? 2 : 4), st);
+    }
+    eng.run(dp, ds, n, dw);
+    std::vector<uint32_t> hw(eng.window_words());
+    HIPX(hipMemcpyAsync(hw.data(), dw, hw.size() * 4, hipMemcpyDeviceToHost, st));
+    HIPX(hipStreamSynchronize(st));
+    const int W = eng.params().windows, c = eng.params().c;
+    if (curve == Curve::G1) {
+      auto a = host::jac_to_aff(fold_windows<HFq>(hw.data(), W, c));
+      *is_inf = a.inf ? 1 : 0;
+      std::memset(out, 0, 64);
+      if (!a.inf) {
+        put_fq(a.x, out);
+        put_fq(a.y, out + 32);
+      }
+    } else {
+      auto a = host::jac_to_aff(fold_windows<HFq2>(hw.data(), W, c));
+      *is_inf = a.inf ? 1 : 0;
+      std::memset(out, 0, 128);
+      if (!a.inf) {
+        put_fq(a.x.c0, out);
+        put_fq(a.x.c1, out + 32);
+        put_fq(a.y.c0, out + 64);
+        put_fq(a.y.c1, out + 96);
+      }
+    }
+  } catch (...) {
+    for (void* p : {(void*)dp, (void*)ds, (void*)dw})
+      if (p) (void)hipFree(p);
+    (void)hipStreamDestroy(st);
+    throw;
+  }
+  for (void* p : {(void*)dp, (void*)ds, (void*)dw})
+    if (p) (void)hipFree(p);
+  HIPX(hipStreamDestroy(st));
+}
+
+void ntt_fr(int device, uint8_t* data, size_t n, int mode) {
+  if (n == 0 || (n & (n - 1))) throw ZkpError(ZKP_ERR_INVALID_ARG, "NTT size must be a power of two");
+  int k = 0;
+  while ((size_t(1) << k) < n) ++k;
+  HIPX(hipSetDevice(device));
+  hipStream_t st;
+  HIPX(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  uint32_t* d = nullptr;
+  try {
+    NttEngine eng(k, st);
+    HIPX(hipMalloc(&d, n * 32));
+    HIPX(hipMemcpyAsync(d, data, n * 32, hipMemcpyHostToDevice, st));
+    launch_fr_to_dev(d, n, st);
+    if (mode == 0)
+      eng.forward(d);
+    else if (mode == 1)
+      eng.inverse(d);
+    else
+      eng.coset_extend(d);
+    launch_fr_from_dev(d, n, st);
+    HIPX(hipMemcpyAsync(data, d, n * 32, hipMemcpyDeviceToHost, st));
+    HIPX(hipStreamSynchronize(st));
+  } catch (...) {
+    if (d) (void)hipFree(d);
+    (void)hipStreamDestroy(st);
+    throw;
+  }
+  HIPX(hipFree(d));
+  HIPX(hipStreamDestroy(st));
+}
+
+}  // namespace zkp

@@ -1,0 +1,89 @@
+// Groth16 prover core (device-resident zkey, per-device pipelines, batch scheduler).
+//
+// Restates snarkjs 0.4.22 groth16_prove MI355X-first:
+//  * load: parse + validate the zkey once, upload the five point sections and
+//    the A/B coefficient matrix (as CSR) to HBM of every device; they stay
+//    resident for the life of the handle (the reference re-reads 3.5 GB per proof).
+//  * prove: only the witness crosses PCIe; buildABC -> 3 x coset NTT -> joinABC
+//    -> 4 G1 MSMs on one stream while the G2 MSM runs on a second stream;
+//    the O(1) tail (window Horner, r/s blinding, affine) runs on the host.
+//  * batch: one host worker thread per device pulls witnesses from a shared
+//    queue (replicas, no collectives: SURVEY.md §8e E1(1)).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <cstddef>
+#include <cstdint>
+#include <memory>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/zkp_amd.h"
+#include "host_ec.hpp"
+#include "msm.hpp"
+#include "ntt.hpp"
+
+namespace zkp {
+
+struct ZkpError : std::runtime_error {
+  zkp_status status;
+  ZkpError(zkp_status s, const std::string& m) : std::runtime_error(m), status(s) {}
+};
+
+struct Section {
+  const uint8_t* ptr = nullptr;
+  uint64_t len = 0;
+};
+
+// Parsed view of a snarkjs binfile (no copies; points into the caller's buffer)
+struct BinFile {
+  uint32_t version = 0;
+  Section sec[16];
+};
+BinFile parse_binfile(const uint8_t* buf, size_t len, const char* magic, uint32_t max_version);
+
+struct ZkeyHeader {
+  uint32_t n_vars = 0, n_public = 0, domain_size = 0, log_domain = 0;
+  uint32_t n_coef = 0;
+  host::Affine<host::Fq> alpha1, beta1, delta1;
+  host::Affine<host::Fq2> beta2, gamma2, delta2;
+};
+
+struct WtnsView {
+  uint32_t n_witness = 0;
+  const uint8_t* values = nullptr;  // n_witness x 32 bytes, standard form LE
+};
+WtnsView parse_wtns(const uint8_t* buf, size_t len);
+
+class DevicePipeline;
+
+class Prover {
+ public:
+  Prover(const uint8_t* zkey, size_t len, const std::vector<int>& devices);
+  ~Prover();
+  const ZkeyHeader& header() const { return hdr_; }
+  // r32/s32 nullable (CSPRNG).  Thread-safe.
+  void prove(const uint8_t* wtns, size_t len, const uint8_t* r32, const uint8_t* s32, zkp_proof* out);
+  void prove_batch(const uint8_t* const* wtns, const size_t* lens, int n, const uint8_t* const* r32s,
+                   const uint8_t* const* s32s, zkp_proof* outs);
+  void quotient(const uint8_t* wtns, size_t len, uint8_t* out);
+  void timings(float* ms, int n) const;
+
+ private:
+  ZkeyHeader hdr_;
+  std::vector<std::unique_ptr<DevicePipeline>> devs_;
+  std::atomic<unsigned> rr_{0};
+  mutable std::mutex tmu_;
+  float last_ms_[7] = {0, 0, 0, 0, 0, 0, 0};
+  friend class DevicePipeline;
+};
+
+// kernel-level helpers (C-ABI zkp_msm_g1/g2, zkp_ntt_fr)
+void msm_points(int device, Curve curve, const uint8_t* points, const uint8_t* scalars, size_t n, uint8_t* out,
+                int* is_inf);
+void ntt_fr(int device, uint8_t* data, size_t n, int mode);
+
+}  // namespace zkp

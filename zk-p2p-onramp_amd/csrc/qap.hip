@@ -1,0 +1,129 @@
+// QAP kernels (see qap.hpp).
+#include "qap.hpp"
+
+#include "field.hpp"
+#include "hip_check.hpp"
+
+namespace zkp {
+
+namespace {
+
+constexpr int TPB = 256;
+inline unsigned grid_for(size_t n) { return (unsigned)((n + TPB - 1) / TPB); }
+
+__global__ __launch_bounds__(TPB) void k_convert_fq_zkey(uint32_t* __restrict__ data, size_t n) {
+  const size_t i = (size_t)blockIdx.x * TPB + threadIdx.x;
+  if (i >= n) return;
+  Fq x = load_fe<FqCfg>(data + i * 8);
+  // Montgomery(2^256) -> Montgomery(2^261): x * 2^266 / 2^261; infinity (0) stays 0
+  x = mul(x, fe_const<FqCfg>(Conv::FQ_ZKEY_TO_DEV));
+  store_fe(data + i * 8, x);
+}
+
+__global__ __launch_bounds__(TPB) void k_convert_coefs(uint32_t* __restrict__ vals, size_t n) {
+  const size_t i = (size_t)blockIdx.x * TPB + threadIdx.x;
+  if (i >= n) return;
+  Fr x = load_fe<FrCfg>(vals + i * 8);
+  x = mul(x, fe_const<FrCfg>(Conv::FR_COEF_TO_DEV));
+  store_fe(vals + i * 8, x);
+}
+
+__device__ __forceinline__ Fr row_dot(const uint32_t* __restrict__ rowptr, const uint32_t* __restrict__ col,
+                                      const uint32_t* __restrict__ val, const uint32_t* __restrict__ w, uint32_t r) {
+  Fr acc = fe_zero<FrCfg>();
+  const uint32_t e1 = rowptr[r + 1];
+  for (uint32_t e = rowptr[r]; e < e1; ++e) {
+    // val = coef*2^522, w standard: mont(val, w) = coef*w*2^261 = Montgomery(coef*w)
+    acc = add(acc, mul(load_fe<FrCfg>(val + (size_t)e * 8), load_fe<FrCfg>(w + (size_t)col[e] * 8)));
+  }
+  return acc;
+}
+
+__global__ __launch_bounds__(TPB) void k_build_abc(const uint32_t* __restrict__ rpa, const uint32_t* __restrict__ cla,
+                                                   const uint32_t* __restrict__ vla, const uint32_t* __restrict__ rpb,
+                                                   const uint32_t* __restrict__ clb, const uint32_t* __restrict__ vlb,
+                                                   const uint32_t* __restrict__ w, uint32_t n, uint32_t* __restrict__ a,
+                                                   uint32_t* __restrict__ b, uint32_t* __restrict__ c) {
+  const uint32_t r = blockIdx.x * TPB + threadIdx.x;
+  if (r >= n) return;
+  Fr av = row_dot(rpa, cla, vla, w, r);
+  Fr bv = row_dot(rpb, clb, vlb, w, r);
+  store_fe(a + (size_t)r * 8, av);
+  store_fe(b + (size_t)r * 8, bv);
+  store_fe(c + (size_t)r * 8, mul(av, bv));
+}
+
+__global__ __launch_bounds__(TPB) void k_join_abc(const uint32_t* __restrict__ a, const uint32_t* __restrict__ b,
+                                                  const uint32_t* __restrict__ c, uint32_t n,
+                                                  uint32_t* __restrict__ p) {
+  const uint32_t j = blockIdx.x * TPB + threadIdx.x;
+  if (j >= n) return;
+  Fr x = sub(mul(load_fe<FrCfg>(a + (size_t)j * 8), load_fe<FrCfg>(b + (size_t)j * 8)),
+             load_fe<FrCfg>(c + (size_t)j * 8));
+  store_fe(p + (size_t)j * 8, from_mont(x));
+}
+
+__global__ __launch_bounds__(TPB) void k_fr_to_dev(uint32_t* __restrict__ d, size_t n) {
+  const size_t i = (size_t)blockIdx.x * TPB + threadIdx.x;
+  if (i >= n) return;
+  store_fe(d + i * 8, to_mont(load_fe<FrCfg>(d + i * 8)));
+}
+
+__global__ __launch_bounds__(TPB) void k_fr_from_dev(uint32_t* __restrict__ d, size_t n) {
+  const size_t i = (size_t)blockIdx.x * TPB + threadIdx.x;
+  if (i >= n) return;
+  store_fe(d + i * 8, from_mont(load_fe<FrCfg>(d + i * 8)));
+}
+
+__global__ __launch_bounds__(TPB) void k_fq_from_dev(uint32_t* __restrict__ d, size_t n) {
+  const size_t i = (size_t)blockIdx.x * TPB + threadIdx.x;
+  if (i >= n) return;
+  store_fe(d + i * 8, from_mont(load_fe<FqCfg>(d + i * 8)));
+}
+
+}  // namespace
+
+void launch_convert_fq_zkey(uint32_t* data, size_t nelems, hipStream_t st) {
+  if (!nelems) return;
+  hipLaunchKernelGGL(k_convert_fq_zkey, dim3(grid_for(nelems)), dim3(TPB), 0, st, data, nelems);
+  HIPX(hipGetLastError());
+}
+
+void launch_convert_coefs(uint32_t* vals, size_t n, hipStream_t st) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_convert_coefs, dim3(grid_for(n)), dim3(TPB), 0, st, vals, n);
+  HIPX(hipGetLastError());
+}
+
+void launch_build_abc(const uint32_t* rpa, const uint32_t* cla, const uint32_t* vla, const uint32_t* rpb,
+                      const uint32_t* clb, const uint32_t* vlb, const uint32_t* w, uint32_t n, uint32_t* a,
+                      uint32_t* b, uint32_t* c, hipStream_t st) {
+  hipLaunchKernelGGL(k_build_abc, dim3(grid_for(n)), dim3(TPB), 0, st, rpa, cla, vla, rpb, clb, vlb, w, n, a, b, c);
+  HIPX(hipGetLastError());
+}
+
+void launch_join_abc(const uint32_t* a, const uint32_t* b, const uint32_t* c, uint32_t n, uint32_t* p,
+                     hipStream_t st) {
+  hipLaunchKernelGGL(k_join_abc, dim3(grid_for(n)), dim3(TPB), 0, st, a, b, c, n, p);
+  HIPX(hipGetLastError());
+}
+
+void launch_fr_to_dev(uint32_t* d, size_t n, hipStream_t st) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_fr_to_dev, dim3(grid_for(n)), dim3(TPB), 0, st, d, n);
+  HIPX(hipGetLastError());
+}
+
+void launch_fr_from_dev(uint32_t* d, size_t n, hipStream_t st) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_fr_from_dev, dim3(grid_for(n)), dim3(TPB), 0, st, d, n);
+  HIPX(hipGetLastError());
+}
+
+void launch_fq_from_dev(uint32_t* d, size_t n, hipStream_t st) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_fq_from_dev, dim3(grid_for(n)), dim3(TPB), 0, st, d, n);
+  HIPX(hipGetLastError());
+}
+
+}  // namespace zkp

@@ -1,0 +1,327 @@
+"""Python host binding of libzkp_amd.so — the MI355X-native Groth16 prover.
+
+Mirrors the snarkjs interface this path replaces (snarkjs@0.4.22, reference
+``package-lock.json:3884-3896``):
+
+* ``groth16.prove(zkeyFileName, witnessFileName, logger=None)`` →
+  ``{"proof": {...}, "publicSignals": [...]}`` — reference call sites
+  ``app/src/helpers/zkp.ts:94`` (via fullProve) and
+  ``dizkus-scripts/5_gen_proof.sh:8`` (CLI).  Inputs are a path or a fastfile
+  memory descriptor ``{"type": "mem", "data": bytes}``.
+* errors raise ``Error`` subclasses with snarkjs' messages ("zkey file is not
+  groth16", "Invalid witness length...", ...).
+
+The HIP library is REQUIRED: there is no CPU fallback.  Loading fails loudly
+(``LibraryNotBuilt``) when ``lib/libzkp_amd.so`` is missing.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+PKG_ROOT = os.path.dirname(_HERE)
+LIB_PATH = os.path.join(PKG_ROOT, "lib", "libzkp_amd.so")
+HEADER_PATH = os.path.join(os.path.dirname(PKG_ROOT), "include", "zkp_amd.h")
+
+ZKP_OK = 0
+STATUS_NAMES = {
+    0: "ZKP_OK", 1: "ZKP_ERR_INVALID_ARG", 2: "ZKP_ERR_IO", 3: "ZKP_ERR_FORMAT", 4: "ZKP_ERR_PROTOCOL",
+    5: "ZKP_ERR_CURVE", 6: "ZKP_ERR_WITNESS_LENGTH", 7: "ZKP_ERR_DEVICE", 8: "ZKP_ERR_OUT_OF_MEMORY",
+    9: "ZKP_ERR_INTERNAL",
+}
+
+
+class LibraryNotBuilt(RuntimeError):
+    pass
+
+
+class ZkpError(Exception):
+    def __init__(self, status: int, message: str):
+        super().__init__("%s: %s" % (STATUS_NAMES.get(status, status), message))
+        self.status = status
+        self.message = message
+
+
+class _Proof(ctypes.Structure):
+    _fields_ = [
+        ("pi_a", (ctypes.c_uint8 * 32) * 2),
+        ("pi_b", ((ctypes.c_uint8 * 32) * 2) * 2),
+        ("pi_c", (ctypes.c_uint8 * 32) * 2),
+        ("n_public", ctypes.c_uint32),
+        ("public_capacity", ctypes.c_uint32),
+        ("public_signals", ctypes.POINTER(ctypes.c_uint8)),
+    ]
+
+
+_lib = None
+_lib_lock = threading.Lock()
+
+
+def load_library(path: str = LIB_PATH):
+    global _lib
+    with _lib_lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(path):
+            raise LibraryNotBuilt("libzkp_amd.so not found at %s — run __graft_entry__.build() "
+                                  "(make -C zk-p2p-onramp_amd)" % path)
+        lib = ctypes.CDLL(path)
+        P = ctypes.c_void_p
+        u8p = ctypes.POINTER(ctypes.c_uint8)
+        sz = ctypes.c_size_t
+        lib.zkp_prover_load_mem.argtypes = [u8p, sz, ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.POINTER(P)]
+        lib.zkp_prover_load_file.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int), ctypes.c_int,
+                                             ctypes.POINTER(P)]
+        lib.zkp_prover_info.argtypes = [P, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32),
+                                        ctypes.POINTER(ctypes.c_uint32)]
+        lib.zkp_prove.argtypes = [P, u8p, sz, u8p, u8p, ctypes.POINTER(_Proof)]
+        lib.zkp_prove_batch.argtypes = [P, ctypes.POINTER(u8p), ctypes.POINTER(sz), ctypes.c_int,
+                                        ctypes.POINTER(u8p), ctypes.POINTER(u8p), ctypes.POINTER(_Proof)]
+        lib.zkp_prove_files.argtypes = [P, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p]
+        lib.zkp_proof_json.argtypes = [ctypes.POINTER(_Proof), ctypes.c_char_p, sz, ctypes.POINTER(sz)]
+        lib.zkp_public_json.argtypes = [ctypes.POINTER(_Proof), ctypes.c_char_p, sz, ctypes.POINTER(sz)]
+        lib.zkp_prover_timings.argtypes = [P, ctypes.POINTER(ctypes.c_float), ctypes.c_int]
+        lib.zkp_prover_free.argtypes = [P]
+        lib.zkp_prover_free.restype = None
+        lib.zkp_last_error.restype = ctypes.c_char_p
+        lib.zkp_version.restype = ctypes.c_char_p
+        lib.zkp_msm_g1.argtypes = [ctypes.c_int, u8p, u8p, sz, u8p, ctypes.POINTER(ctypes.c_int)]
+        lib.zkp_msm_g2.argtypes = [ctypes.c_int, u8p, u8p, sz, u8p, ctypes.POINTER(ctypes.c_int)]
+        lib.zkp_ntt_fr.argtypes = [ctypes.c_int, u8p, sz, ctypes.c_int]
+        lib.zkp_quotient.argtypes = [P, u8p, sz, u8p]
+        for name in ("zkp_prover_load_mem", "zkp_prover_load_file", "zkp_prover_info", "zkp_prove",
+                     "zkp_prove_batch", "zkp_prove_files", "zkp_proof_json", "zkp_public_json",
+                     "zkp_prover_timings", "zkp_msm_g1", "zkp_msm_g2", "zkp_ntt_fr", "zkp_quotient"):
+            getattr(lib, name).restype = ctypes.c_int
+        _lib = lib
+        return lib
+
+
+def _check(st: int):
+    if st != ZKP_OK:
+        raise ZkpError(st, load_library().zkp_last_error().decode())
+
+
+def _buf(data: bytes):
+    """(ctypes uint8 pointer, keepalive) for an immutable bytes-like object."""
+    arr = (ctypes.c_uint8 * len(data)).from_buffer_copy(data) if len(data) else (ctypes.c_uint8 * 1)()
+    return ctypes.cast(arr, ctypes.POINTER(ctypes.c_uint8)), arr
+
+
+def _le(b) -> int:
+    return int.from_bytes(bytes(b), "little")
+
+
+def version() -> str:
+    return load_library().zkp_version().decode()
+
+
+class Prover:
+    """A zkey resident in HBM of one or more devices (loaded once, reused per proof)."""
+
+    def __init__(self, zkey, devices=None):
+        lib = load_library()
+        h = ctypes.c_void_p()
+        devs = list(devices or [])
+        darr = (ctypes.c_int * max(1, len(devs)))(*devs) if devs else None
+        dptr = ctypes.cast(darr, ctypes.POINTER(ctypes.c_int)) if darr is not None else None
+        if isinstance(zkey, (bytes, bytearray, memoryview)):
+            p, keep = _buf(bytes(zkey))
+            _check(lib.zkp_prover_load_mem(p, len(zkey), dptr, len(devs), ctypes.byref(h)))
+            del keep
+        else:
+            _check(lib.zkp_prover_load_file(os.fsencode(zkey), dptr, len(devs), ctypes.byref(h)))
+        self._h = h
+        nv, npub, dom = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
+        _check(lib.zkp_prover_info(h, ctypes.byref(nv), ctypes.byref(npub), ctypes.byref(dom)))
+        self.n_vars, self.n_public, self.domain_size = nv.value, npub.value, dom.value
+
+    def close(self):
+        if getattr(self, "_h", None):
+            load_library().zkp_prover_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _new_proof(self):
+        pub = (ctypes.c_uint8 * (32 * max(1, self.n_public)))()
+        pr = _Proof()
+        pr.public_capacity = self.n_public
+        pr.public_signals = ctypes.cast(pub, ctypes.POINTER(ctypes.c_uint8))
+        return pr, pub
+
+    @staticmethod
+    def _scalar(x):
+        if x is None:
+            return None, None
+        return _buf(int(x).to_bytes(32, "little"))
+
+    def prove_raw(self, wtns: bytes, r=None, s=None):
+        """Returns ((ax, ay), ((bx0, bx1), (by0, by1)), (cx, cy)), [public ints]."""
+        lib = load_library()
+        wp, wk = _buf(wtns)
+        rp, rk = self._scalar(r)
+        sp, sk = self._scalar(s)
+        pr, pub = self._new_proof()
+        _check(lib.zkp_prove(self._h, wp, len(wtns), rp, sp, ctypes.byref(pr)))
+        return _unpack_proof(pr, pub)
+
+    def prove_batch_raw(self, wtns_list, rs=None, ss=None):
+        lib = load_library()
+        n = len(wtns_list)
+        keep = []
+        wps = (ctypes.POINTER(ctypes.c_uint8) * n)()
+        lens = (ctypes.c_size_t * n)()
+        for i, w in enumerate(wtns_list):
+            p, k = _buf(w)
+            keep.append(k)
+            wps[i] = p
+            lens[i] = len(w)
+
+        def arr(vals):
+            if vals is None:
+                return None
+            a = (ctypes.POINTER(ctypes.c_uint8) * n)()
+            for i, v in enumerate(vals):
+                p, k = _buf(int(v).to_bytes(32, "little"))
+                keep.append(k)
+                a[i] = p
+            return a
+
+        ra, sa = arr(rs), arr(ss)
+        proofs = (_Proof * n)()
+        pubs = []
+        for i in range(n):
+            pub = (ctypes.c_uint8 * (32 * max(1, self.n_public)))()
+            pubs.append(pub)
+            proofs[i].public_capacity = self.n_public
+            proofs[i].public_signals = ctypes.cast(pub, ctypes.POINTER(ctypes.c_uint8))
+        _check(lib.zkp_prove_batch(self._h, wps, lens, n, ra, sa, proofs))
+        return [_unpack_proof(proofs[i], pubs[i]) for i in range(n)]
+
+    def prove(self, wtns: bytes, r=None, s=None):
+        """snarkjs-shaped result {"proof": {...}, "publicSignals": [...]} (decimal strings)."""
+        (a, b, c), pub = self.prove_raw(wtns, r, s)
+        return {"proof": proof_object(a, b, c), "publicSignals": [str(x) for x in pub]}
+
+    def quotient(self, wtns: bytes):
+        lib = load_library()
+        wp, wk = _buf(wtns)
+        out = (ctypes.c_uint8 * (32 * self.domain_size))()
+        _check(lib.zkp_quotient(self._h, wp, len(wtns), ctypes.cast(out, ctypes.POINTER(ctypes.c_uint8))))
+        raw = bytes(out)
+        return [_le(raw[32 * i:32 * i + 32]) for i in range(self.domain_size)]
+
+    def timings(self):
+        lib = load_library()
+        ms = (ctypes.c_float * 7)()
+        _check(lib.zkp_prover_timings(self._h, ms, 7))
+        keys = ["wtns_h2d", "build_abc", "ntt_quotient", "msm_g1", "msm_g2", "host_assembly", "total_wall"]
+        return dict(zip(keys, list(ms)))
+
+    def prove_files(self, wtns_path, proof_path, public_path):
+        _check(load_library().zkp_prove_files(self._h, os.fsencode(wtns_path), os.fsencode(proof_path),
+                                              os.fsencode(public_path)))
+
+
+def _unpack_proof(pr, pub):
+    a = (_le(pr.pi_a[0]), _le(pr.pi_a[1]))
+    b = ((_le(pr.pi_b[0][0]), _le(pr.pi_b[0][1])), (_le(pr.pi_b[1][0]), _le(pr.pi_b[1][1])))
+    c = (_le(pr.pi_c[0]), _le(pr.pi_c[1]))
+    raw = bytes(pub)
+    signals = [_le(raw[32 * i:32 * i + 32]) for i in range(pr.n_public)]
+    return (a, b, c), signals
+
+
+def proof_object(a, b, c) -> dict:
+    """snarkjs proof object (groth16_prove: pi_a, pi_b, pi_c, protocol, curve)."""
+    return {
+        "pi_a": [str(a[0]), str(a[1]), "1"],
+        "pi_b": [[str(b[0][0]), str(b[0][1])], [str(b[1][0]), str(b[1][1])], ["1", "0"]],
+        "pi_c": [str(c[0]), str(c[1]), "1"],
+        "protocol": "groth16",
+        "curve": "bn128",
+    }
+
+
+# ---------------------------------------------------------------- snarkjs-style module API
+
+def _read_input(x) -> bytes:
+    if isinstance(x, dict) and x.get("type") == "mem":
+        return bytes(x["data"])
+    if isinstance(x, (bytes, bytearray, memoryview)):
+        return bytes(x)
+    with open(x, "rb") as f:
+        return f.read()
+
+
+class _Groth16:
+    """``groth16.prove`` with a per-process cache of loaded (HBM-resident) zkeys."""
+
+    def __init__(self):
+        self._cache = {}
+        self._lock = threading.Lock()
+
+    def _prover(self, zkey):
+        key = zkey if isinstance(zkey, str) else id(zkey)
+        with self._lock:
+            p = self._cache.get(key)
+            if p is None:
+                p = Prover(zkey if isinstance(zkey, str) else _read_input(zkey))
+                self._cache[key] = p
+            return p
+
+    def prove(self, zkeyFileName, witnessFileName, logger=None, r=None, s=None):
+        p = self._prover(zkeyFileName)
+        if logger is not None:
+            logger.debug("zkp_amd: proving on device (nVars=%d, domain=%d)" % (p.n_vars, p.domain_size))
+        return p.prove(_read_input(witnessFileName), r=r, s=s)
+
+
+groth16 = _Groth16()
+
+
+def msm_g1(points_lem: bytes, scalars_le: bytes, device: int = 0):
+    """Kernel-level G1 MSM: zkey-layout points, 32-byte LE scalars -> affine (x, y) or None."""
+    lib = load_library()
+    n = len(scalars_le) // 32
+    pp, pk = _buf(points_lem)
+    sp, sk = _buf(scalars_le)
+    out = (ctypes.c_uint8 * 64)()
+    inf = ctypes.c_int()
+    _check(lib.zkp_msm_g1(device, pp, sp, n, ctypes.cast(out, ctypes.POINTER(ctypes.c_uint8)), ctypes.byref(inf)))
+    if inf.value:
+        return None
+    raw = bytes(out)
+    return (_le(raw[:32]), _le(raw[32:]))
+
+
+def msm_g2(points_lem: bytes, scalars_le: bytes, device: int = 0):
+    lib = load_library()
+    n = len(scalars_le) // 32
+    pp, pk = _buf(points_lem)
+    sp, sk = _buf(scalars_le)
+    out = (ctypes.c_uint8 * 128)()
+    inf = ctypes.c_int()
+    _check(lib.zkp_msm_g2(device, pp, sp, n, ctypes.cast(out, ctypes.POINTER(ctypes.c_uint8)), ctypes.byref(inf)))
+    if inf.value:
+        return None
+    raw = bytes(out)
+    v = [_le(raw[32 * i:32 * i + 32]) for i in range(4)]
+    return ((v[0], v[1]), (v[2], v[3]))
+
+
+def ntt_fr(values, mode: int, device: int = 0):
+    """mode 0 forward, 1 inverse, 2 coset-extend (snarkjs ifft -> applyKey -> fft)."""
+    lib = load_library()
+    raw = b"".join(int(v).to_bytes(32, "little") for v in values)
+    arr = (ctypes.c_uint8 * len(raw)).from_buffer_copy(raw)
+    _check(lib.zkp_ntt_fr(device, ctypes.cast(arr, ctypes.POINTER(ctypes.c_uint8)), len(values), mode))
+    out = bytes(arr)
+    return [_le(out[32 * i:32 * i + 32]) for i in range(len(values))]
