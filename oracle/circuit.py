@@ -7,8 +7,10 @@ benchmarks run on synthetic circuits with the Venmo circuit's *shape*
 constraint, and a witness that is mostly bits like a SHA/regex circuit
 (``circuit/circuit.circom:62-134``).  The witness distribution is an ASSUMPTION.
 
-Construction (deterministic from ``seed``; mirrored bit-for-bit by the C++
-generator ``zk-p2p-onramp_amd/csrc/synth.cpp`` — tests compare the two):
+Construction (mirrored bit-for-bit by the C++ generator
+``zk-p2p-onramp_amd/csrc/synth/synth.hip`` — tests compare the two): the circuit
+STRUCTURE comes from stream 3 of ``seed``; the witness's free inputs from stream 4
+of ``wseed``, so many distinct witnesses share one circuit (batch benchmarks).
 
 * w0 = 1; public w1..w_nPublic = random u64 values (packed-limb-like).
 * the first ``n_in`` private signals are free input bits.
@@ -75,32 +77,27 @@ def _lc(pairs):
     return sorted((s, c) for s, c in d.items() if c != 0)
 
 
-def gen_circuit(n_vars: int, n_constraints: int, n_public: int, seed: int, in_permille: int = 50):
-    """Returns (R1CS, witness).  Requires n_constraints >= n_vars - 1 - n_public - n_in."""
+def gen_program(n_vars: int, n_constraints: int, n_public: int, seed: int, in_permille: int = 50):
+    """Circuit STRUCTURE from stream 3 of ``seed``: (R1CS, program).  program is the
+    list of defining steps used by ``gen_witness``; nothing here depends on values."""
     rng = SplitMix64(seed, 3)
     n_priv = n_vars - 1 - n_public
     n_in = max(2, n_priv * in_permille // 1000)
     if n_priv < n_in:
         raise ValueError("too few private signals")
-    w = [1]
-    for _ in range(n_public):
-        w.append(rng.next())
-    bits = []
-    for k in range(n_in):
-        v = 1 + n_public + k
-        w.append(rng.next() & 1)
-        bits.append(v)
+    bits = [1 + n_public + k for k in range(n_in)]
     cons = []
+    prog = []
     for v in range(1 + n_public + n_in, n_vars):
         x = rng.below(100)
         if x < 70:
             a = bits[rng.below(len(bits))]
             b = bits[rng.below(len(bits))]
             if x < 35:
-                w.append(w[a] * w[b])
+                prog.append((0, a, b))
                 cons.append((_lc([(a, 1)]), _lc([(b, 1)]), _lc([(v, 1)])))
             else:
-                w.append((w[a] + w[b] - 2 * w[a] * w[b]) % R)
+                prog.append((1, a, b))
                 cons.append((_lc([(a, 2)]), _lc([(b, 1)]), _lc([(a, 1), (b, 1), (v, R - 1)])))
             bits.append(v)
         else:
@@ -108,7 +105,7 @@ def gen_circuit(n_vars: int, n_constraints: int, n_public: int, seed: int, in_pe
             b = rng.below(v)
             c = rng.below(v)
             c1, c2, c3, c4 = rng.fr(), rng.fr(), rng.fr(), rng.fr()
-            w.append((c1 * w[a] + c2 * w[b]) * (c3 * w[c] + c4) % R)
+            prog.append((2, a, b, c, c1, c2, c3, c4))
             cons.append((_lc([(a, c1), (b, c2)]), _lc([(c, c3), (0, c4)]), _lc([(v, 1)])))
     if len(cons) > n_constraints:
         raise ValueError("n_constraints too small for n_vars")
@@ -117,7 +114,36 @@ def gen_circuit(n_vars: int, n_constraints: int, n_public: int, seed: int, in_pe
         b = bits[i] if i < n_in else bits[rng.below(len(bits))]
         i += 1
         cons.append((_lc([(b, 1)]), _lc([(b, 1), (0, R - 1)]), []))
-    return R1CS(n_vars, n_public, n_constraints, cons), w
+    meta = {"n_public": n_public, "n_in": n_in}
+    return R1CS(n_vars, n_public, n_constraints, cons), (meta, prog)
+
+
+def gen_witness(program, wseed: int):
+    """Witness from stream 4 of ``wseed``: public values (u64) and input bits are
+    free; every other signal is computed by its defining constraint."""
+    meta, prog = program
+    rng = SplitMix64(wseed, 4)
+    w = [1]
+    for _ in range(meta["n_public"]):
+        w.append(rng.next())
+    for _ in range(meta["n_in"]):
+        w.append(rng.next() & 1)
+    for step in prog:
+        if step[0] == 0:
+            w.append(w[step[1]] * w[step[2]])
+        elif step[0] == 1:
+            a, b = w[step[1]], w[step[2]]
+            w.append((a + b - 2 * a * b) % R)
+        else:
+            _, a, b, c, c1, c2, c3, c4 = step
+            w.append((c1 * w[a] + c2 * w[b]) * (c3 * w[c] + c4) % R)
+    return w
+
+
+def gen_circuit(n_vars: int, n_constraints: int, n_public: int, seed: int, in_permille: int = 50, wseed=None):
+    """Returns (R1CS, witness); the witness uses ``wseed`` (default: ``seed``)."""
+    r1cs, prog = gen_program(n_vars, n_constraints, n_public, seed, in_permille)
+    return r1cs, gen_witness(prog, seed if wseed is None else wseed)
 
 
 def check_witness(r1cs: R1CS, w) -> bool:
