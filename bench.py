@@ -1,0 +1,245 @@
+#!/usr/bin/env python3
+"""Headline benchmark: Groth16 proofs/s for the Venmo-shaped circuit on MI355X.
+
+BASELINE.json metric: "Groth16 proofs/sec (node) + 1-proof latency, Venmo circuit;
+G1 MSM Mpts/s".  Workload at N=1 = configs[2] (full Venmo-circuit proof on one
+MI355X); the circuit is SYNTHETIC with the Venmo shape (nVars 6,400,562,
+nConstraints 6,618,823, nPublic 26, domain 2^23) because the
+real 3.5 GB zkey / witness are absent.  Insecure known-tau setup.
+
+A "step" = one complete proof (buildABC, 3 coset NTTs, joinABC, 4 G1 + 1 G2 MSMs,
+blinding) of one distinct synthetic witness already resident in HBM (staged).
+Multi-GPU (torchrun --nproc-per-node N): every rank proves its own witnesses on its
+own GPU (replicas, no collectives: SURVEY.md §8e E1(1)); value = all proofs / max
+rank time.  Extra fields: latency, per-stage ms, config-2 kernels (G1 MSM 2^20
+Mpts/s, Fr NTT 2^20), roofline of the bucket-accumulate kernel (HIP events), and
+the C++ CPU restatement (oracle/cpu) timed on this host as cpu_baseline.
+"""
+import argparse
+import json
+import os
+import sys
+import threading
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "zk-p2p-onramp_amd"))
+
+import zkp_amd  # noqa: E402
+from zkp_amd import synth  # noqa: E402
+
+CIRCUIT_SEED = 0x5A4B5032
+SETUP_SEED = 0x5A4B5033
+# Measured on MI355X by tools/ubench/int_mul_rate (profiles/ubench_r01.txt): v_mad_u64_u32
+# throughput, the instruction every 32x32->64 partial product of the field multiply maps to.
+MAD_PEAK_TOPS = None  # filled from profiles/ubench_r01.json when present
+MAC_PER_FPMUL = 136     # SURVEY.md §8d D4 (8x32-bit CIOS: 64 + 64 + 8)
+FPMUL_PER_MADD = 11     # SURVEY.md §8d D4 (mixed Jacobian add 7M + 4S)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def load_peak():
+    p = os.path.join(ROOT, "profiles", "ubench_r01.json")
+    try:
+        with open(p) as f:
+            return json.load(f)["v_mad_u64_u32_tops"], p
+    except Exception:
+        return None, None
+
+
+def load_traffic():
+    p = os.path.join(ROOT, "profiles", "pmc_accumulate_r01.json")
+    try:
+        with open(p) as f:
+            return json.load(f)
+    except Exception:
+        return None
+
+
+def gen_witnesses(circ, seeds):
+    out = [None] * len(seeds)
+
+    def work(i):
+        out[i] = circ.witness(seeds[i])
+
+    ths = [threading.Thread(target=work, args=(i,)) for i in range(len(seeds))]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    return out
+
+
+def kernel_benches(device, log_n=20, iters=10):
+    """configs[1]: G1 MSM 2^20 (uniform scalars) + Fr NTT 2^20, device-resident."""
+    n = 1 << log_n
+    sc_pts = synth.scalars(CIRCUIT_SEED, 0, n)
+    pts = synth.points(sc_pts, g2=False, device=device)
+    scal = synth.scalars(CIRCUIT_SEED, 1, n)
+    st, res = zkp_amd.bench_msm(pts, scal, g2=False, warmup=2, iters=iters, device=device)
+    ntt_ms = zkp_amd.bench_ntt(log_n, warmup=2, iters=iters, device=device)
+    return {
+        "msm_g1_2^20_ms": round(st["ms_per_msm"], 3),
+        "msm_g1_2^20_Mpts_per_s": round(n / st["ms_per_msm"] / 1e3, 1),
+        "msm_g1_2^20_accumulate_ms": round(st["ms_accumulate"], 3),
+        "msm_window_bits": st["c"],
+        "ntt_fr_2^20_coset_extend_ms": round(ntt_ms, 3),
+    }, st
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=8)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--witnesses", type=int, default=4, help="distinct staged witnesses per rank (cycled)")
+    ap.add_argument("--cpu-baseline", choices=["full", "none"], default="full")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-kernels", action="store_true")
+    ap.add_argument("--scale", type=float, default=1.0, help="fraction of the Venmo shape (smoke/debug only)")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # noqa: F811
+        dist.init_process_group("gloo")  # measurement plumbing only (barrier / max); the path has no collective
+
+    t_setup = time.time()
+    if args.scale == 1.0:
+        circ = synth.Circuit.venmo(CIRCUIT_SEED)
+    else:
+        v = synth.VENMO
+        circ = synth.Circuit(int(v["n_vars"] * args.scale), int(v["n_constraints"] * args.scale), v["n_public"],
+                             CIRCUIT_SEED)
+    nw = max(1, min(args.witnesses, args.steps + args.warmup))
+    wseeds = [1000 * rank + i + 1 for i in range(nw)]
+    wit = gen_witnesses(circ, wseeds)
+    log("[rank %d] circuit + %d witnesses: %.1fs" % (rank, nw, time.time() - t_setup))
+    t0 = time.time()
+    zk = circ.zkey(SETUP_SEED, device=local)
+    log("[rank %d] synthetic zkey (%.2f GB): %.1fs" % (rank, zk.len / 1e9, time.time() - t0))
+    t0 = time.time()
+    prover = zkp_amd.Prover(zk, devices=[local])
+    for i, w in enumerate(wit):
+        prover.stage(w, slot=i)
+    log("[rank %d] zkey resident in HBM + witnesses staged: %.1fs" % (rank, time.time() - t0))
+
+    R_FIX, S_FIX = 0x1234567, 0x7654321
+    for i in range(args.warmup):
+        prover.prove_staged_raw(i % nw, R_FIX, S_FIX)
+    prover.instrument(True)
+
+    def sync():
+        try:
+            import torch
+            if torch.cuda.is_available():
+                torch.cuda.synchronize(local)
+        except Exception:
+            pass
+
+    if dist:
+        dist.barrier()
+    sync()
+    t_start = time.perf_counter()
+    results = []
+    for i in range(args.steps):
+        results.append(prover.prove_staged_raw(i % nw, R_FIX, S_FIX))
+    sync()
+    elapsed = time.perf_counter() - t_start
+    if dist:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        dist.barrier()
+    kstats = prover.kernel_stats()
+    stage_ms = prover.timings()
+
+    # H2D-inclusive latency of one proof from a host witness (reported beside, never `value`)
+    t0 = time.perf_counter()
+    prover.prove_raw(wit[0], R_FIX, S_FIX)
+    pcie_latency_ms = (time.perf_counter() - t0) * 1e3
+
+    if rank != 0:
+        return
+
+    n_total = args.steps * world
+    value = n_total / elapsed
+    ms_per_step = elapsed / args.steps * 1e3
+    g1 = kstats["g1"]
+    acc_ms = g1["accumulate_ms"] / max(1, g1["launches"])
+    adds = g1["mixed_adds"] / max(1, g1["launches"])
+    peak, peak_src = load_peak()
+    achieved = adds * FPMUL_PER_MADD * MAC_PER_FPMUL / (acc_ms * 1e-3) / 1e12 if acc_ms > 0 else None
+    traffic = load_traffic()
+    roofline = {
+        "kernel": "k_accumulate<Fq> (G1 bucket accumulation, XYZZ mixed adds)",
+        "bound": "valu-int",
+        "achieved": round(achieved, 3) if achieved else None,
+        "peak": peak,
+        "unit": "TMAC/s (32x32->64 v_mad_u64_u32)",
+        "frac": round(achieved / peak, 4) if (achieved and peak) else None,
+        "traffic": traffic.get("hbm_bytes_per_launch") if traffic else None,
+        "algorithmic_work_per_launch": {"mixed_adds": int(adds), "fp_mul_per_add": FPMUL_PER_MADD,
+                                        "mac_per_fp_mul": MAC_PER_FPMUL},
+        "avg_launch_ms": round(acc_ms, 4),
+        "launches_timed": g1["launches"],
+        "peak_source": peak_src,
+    }
+
+    out = {
+        "metric": "Groth16 proofs/sec (node) + 1-proof latency, Venmo circuit; G1 MSM Mpts/s",
+        "value": round(value, 4),
+        "unit": "proofs/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 3),
+        "latency_ms": round(ms_per_step, 3),
+        "latency_ms_pcie_inclusive": round(pcie_latency_ms, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32-limb Fp/Fr (BN254 integer arithmetic)",
+        "data": "synthetic Venmo-shaped circuit + distinct synthetic witnesses, insecure known-tau zkey",
+        "config": {"workload": "configs[2]: full Groth16 prove, Venmo-shaped circuit, 1 proof per step",
+                   "n_vars": circ.n_vars, "n_constraints": circ.n_constraints, "n_public": circ.n_public,
+                   "domain": circ.domain_size, "distinct_witnesses_per_rank": nw,
+                   "parallelism": "replicas%d" % world},
+        "stage_ms_last_proof": {k: round(v, 3) for k, v in stage_ms.items()},
+        "roofline": roofline,
+    }
+
+    if not args.no_kernels:
+        kb, _ = kernel_benches(local)
+        out["kernels_config1"] = kb
+
+    if args.cpu_baseline == "full":
+        try:
+            from oracle import cpu_oracle
+            t0 = time.time()
+            (ca, cb, cc), cms = cpu_oracle.prove(None, wit[0], R_FIX, S_FIX, threads=args.cpu_threads,
+                                                  zkey_ptr=zk.ptr, zkey_len=zk.len)
+            cpu_s = time.time() - t0
+            gpu_proof = results[0][0]
+            out["cpu_baseline"] = {
+                "value": round(1.0 / cpu_s, 5), "unit": "proofs/s", "cores": args.cpu_threads, "kind": "port",
+                "sample": "one full Venmo-shaped proof (same zkey/witness 0) by oracle/cpu C++ restatement, "
+                          "%d threads: %.1f s (abc %.0f, ntt %.0f, g1 %.0f, g2 %.0f ms)" % (
+                              args.cpu_threads, cpu_s, cms[0], cms[1], cms[2], cms[3]),
+                "bit_exact_vs_gpu": (ca, cb, cc) == gpu_proof,
+            }
+        except Exception as e:  # reported, never silently replaced
+            out["cpu_baseline"] = {"value": None, "error": str(e)}
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

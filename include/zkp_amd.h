@@ -114,6 +114,25 @@ zkp_status zkp_ntt_fr(int device, uint8_t* data, size_t n, int mode);
 /* The H-MSM scalars P_j (standard form, n = domain) for (zkey, wtns): rows A4..A8. */
 zkp_status zkp_quotient(zkp_prover* p, const uint8_t* wtns, size_t len, uint8_t* out);
 
+/* ---- benchmarking / serving helpers ----
+ * Keep a witness resident in HBM (device index into the prover's device list, any
+ * slot number); zkp_prove_staged then runs the proof without the PCIe copy. */
+zkp_status zkp_witness_stage(zkp_prover* p, int dev_index, int slot, const uint8_t* wtns, size_t len);
+zkp_status zkp_prove_staged(zkp_prover* p, int dev_index, int slot, const uint8_t* r32, const uint8_t* s32,
+                            zkp_proof* out);
+/* Bracket every bucket-accumulate kernel launch with HIP events (on its stream).
+ * zkp_prover_kernel_stats: [0] G1 accumulate ms (sum), [1] G1 launches, [2] G1 mixed
+ * additions, [3] G1 tasks, [4..7] the same for G2.  Enabling resets the counters. */
+zkp_status zkp_prover_instrument(zkp_prover* p, int on);
+zkp_status zkp_prover_kernel_stats(const zkp_prover* p, double* out, int n);
+/* Device-resident kernel benchmarks.  MSM: stats[0] ms per MSM, [1] ms per
+ * accumulate-kernel launch, [2] mixed additions per launch, [3] tasks per launch,
+ * [4] window bits c, [5] windows.  out/is_inf receive the result (verification). */
+zkp_status zkp_bench_msm(int device, int g2, const uint8_t* points, const uint8_t* scalars, size_t n, int warmup,
+                         int iters, double* stats, uint8_t* out, int* is_inf);
+/* ms per coset-extension (iNTT + coset key + NTT) of 2^log_n Fr elements */
+zkp_status zkp_bench_ntt(int device, int log_n, int warmup, int iters, double* ms);
+
 #ifdef __cplusplus
 }
 #endif

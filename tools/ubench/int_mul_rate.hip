@@ -10,7 +10,7 @@
   fprintf(stderr, "HIP error %s at %s:%d\n", hipGetErrorString(e), __FILE__, __LINE__); return 1; } } while (0)
 
 constexpr int ITERS = 4096;
-constexpr int CHAINS = 8;
+constexpr int CHAINS = 16;
 
 // v_mad_u64_u32: acc = a * b + acc (64-bit accumulate)
 __global__ void k_mad_u64(uint64_t* out, uint32_t seed) {
@@ -274,6 +274,24 @@ int main() {
   if (run("v_fma_f64", k_fma_f64, d, blocks, threads)) return 1;
   for (int bm : {1, 2, 4, 8}) { uint64_t* d2; CHK(hipMalloc(&d2, (size_t)prop.multiProcessorCount * bm * 256 * 8)); if (run_mont(d2, prop.multiProcessorCount * bm, 256)) return 1; CHK(hipFree(d2)); }
   for (int bm : {1, 2, 4, 8}) { uint64_t* d2; CHK(hipMalloc(&d2, (size_t)prop.multiProcessorCount * bm * 256 * 8)); if (run_mont29(d2, prop.multiProcessorCount * bm, 256)) return 1; CHK(hipFree(d2)); }
+  // summary line consumed by bench.py (profiles/ubench_r01.json): best v_mad_u64_u32 rate over occupancies
+  double best = 0;
+  for (int bm : {4, 8, 16}) {
+    uint64_t* d2; CHK(hipMalloc(&d2, (size_t)prop.multiProcessorCount * bm * 256 * 8));
+    hipEvent_t e0, e1; CHK(hipEventCreate(&e0)); CHK(hipEventCreate(&e1));
+    hipLaunchKernelGGL(k_mad_u64, dim3(prop.multiProcessorCount * bm), dim3(256), 0, 0, d2, 1u);
+    CHK(hipDeviceSynchronize());
+    for (int r = 0; r < 5; ++r) {
+      CHK(hipEventRecord(e0));
+      hipLaunchKernelGGL(k_mad_u64, dim3(prop.multiProcessorCount * bm), dim3(256), 0, 0, d2, (uint32_t)r);
+      CHK(hipEventRecord(e1)); CHK(hipEventSynchronize(e1));
+      float ms; CHK(hipEventElapsedTime(&ms, e0, e1));
+      double tops = (double)prop.multiProcessorCount * bm * 256 * ITERS * CHAINS / (ms * 1e-3) / 1e12;
+      if (tops > best) best = tops;
+    }
+    CHK(hipFree(d2));
+  }
+  printf("{\"summary\": true, \"v_mad_u64_u32_tops\": %.3f, \"chains_per_lane\": %d}\n", best, CHAINS);
   CHK(hipFree(d));
   return 0;
 }

@@ -215,4 +215,41 @@ zkp_status zkp_quotient(zkp_prover* p, const uint8_t* wtns, size_t len, uint8_t*
   return guard([&] { p->impl->quotient(wtns, len, out); });
 }
 
+zkp_status zkp_witness_stage(zkp_prover* p, int dev_index, int slot, const uint8_t* wtns, size_t len) {
+  if (!p || !wtns) return fail(ZKP_ERR_INVALID_ARG, "null argument");
+  return guard([&] { p->impl->stage(dev_index, slot, wtns, len); });
+}
+
+zkp_status zkp_prove_staged(zkp_prover* p, int dev_index, int slot, const uint8_t* r32, const uint8_t* s32,
+                            zkp_proof* out) {
+  if (!p || !out) return fail(ZKP_ERR_INVALID_ARG, "null argument");
+  return guard([&] { p->impl->prove_staged(dev_index, slot, r32, s32, out); });
+}
+
+zkp_status zkp_prover_instrument(zkp_prover* p, int on) {
+  if (!p) return fail(ZKP_ERR_INVALID_ARG, "null prover");
+  return guard([&] { p->impl->set_instrument(on != 0); });
+}
+
+zkp_status zkp_prover_kernel_stats(const zkp_prover* p, double* out, int n) {
+  if (!p || !out) return fail(ZKP_ERR_INVALID_ARG, "null argument");
+  return guard([&] { p->impl->kernel_stats(out, n); });
+}
+
+zkp_status zkp_bench_msm(int device, int g2, const uint8_t* points, const uint8_t* scalars, size_t n, int warmup,
+                         int iters, double* stats, uint8_t* out, int* is_inf) {
+  if (!points || !scalars || !stats) return fail(ZKP_ERR_INVALID_ARG, "null argument");
+  return guard([&] {
+    zkp::MsmBench b = zkp::bench_msm(device, g2 ? zkp::Curve::G2 : zkp::Curve::G1, points, scalars, n, warmup,
+                                     iters, out, is_inf);
+    stats[0] = b.ms_per_msm, stats[1] = b.ms_accumulate, stats[2] = (double)b.mixed_adds;
+    stats[3] = (double)b.tasks, stats[4] = b.c, stats[5] = b.windows;
+  });
+}
+
+zkp_status zkp_bench_ntt(int device, int log_n, int warmup, int iters, double* ms) {
+  if (!ms || log_n < 1 || log_n > 27) return fail(ZKP_ERR_INVALID_ARG, "bad argument");
+  return guard([&] { *ms = zkp::bench_ntt(device, log_n, warmup, iters); });
+}
+
 }  // extern "C"

@@ -124,9 +124,32 @@ MsmEngine::MsmEngine(Curve curve, size_t max_n, hipStream_t stream)
   HIPX(hipMalloc(&sort_tmp_, sort_tmp_bytes_));
   HIPX(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_tmp_bytes_, cnt_, off_a_, (int)(nbuckets_ + 1), stream_));
   HIPX(hipMalloc(&scan_tmp_, scan_tmp_bytes_));
+  for (auto& e : ev_) {
+    HIPX(hipEventCreate(&e[0]));
+    HIPX(hipEventCreate(&e[1]));
+  }
+  HIPX(hipHostMalloc(&h_counts_, MAX_PENDING * 3 * 4, hipHostMallocDefault));
+}
+
+void MsmEngine::collect(Stats& s) {
+  for (int i = 0; i < pending_; ++i) {
+    float ms = 0;
+    HIPX(hipEventElapsedTime(&ms, ev_[i][0], ev_[i][1]));
+    s.accumulate_ms += ms;
+    s.launches += 1;
+    const uint32_t inv_start = h_counts_[3 * i], inv_end = h_counts_[3 * i + 1];
+    s.mixed_adds += inv_end ? inv_start : h_total_[i];
+    s.tasks += h_counts_[3 * i + 2];
+  }
+  pending_ = 0;
 }
 
 MsmEngine::~MsmEngine() {
+  for (auto& e : ev_) {
+    (void)hipEventDestroy(e[0]);
+    (void)hipEventDestroy(e[1]);
+  }
+  if (h_counts_) (void)hipHostFree(h_counts_);
   for (void* p : {(void*)keys_, (void*)vals_, (void*)keys_sorted_, (void*)vals_sorted_, (void*)bstart_, (void*)bend_,
                   (void*)cnt_, (void*)off_a_, (void*)off_b_, (void*)part_a_, (void*)part_b_, (void*)buckets_,
                   (void*)lvl_s_[0], (void*)lvl_s_[1], (void*)lvl_t_[0], (void*)lvl_t_[1], sort_tmp_, scan_tmp_})
@@ -160,12 +183,22 @@ void MsmEngine::run(const uint32_t* points, const uint32_t* scalars, size_t n, u
     size_t stmp = scan_tmp_bytes_;
     HIPX(hipcub::DeviceScan::ExclusiveSum(scan_tmp_, stmp, cnt_, off_a_, (int)(nbuckets_ + 1), st));
     const size_t max_tasks_now = ((size_t)total + prm_.S - 1) / prm_.S + nbuckets_;
+    const int slot = (instrument_ && pending_ < MAX_PENDING) ? pending_++ : -1;
+    if (slot >= 0) HIPX(hipEventRecord(ev_[slot][0], st));
     if (curve_ == Curve::G1)
       launch_accumulate<Fq>(points, vals_sorted_, bstart_, bend_, off_a_, nb, (uint32_t)prm_.S, part_a_,
                             max_tasks_now, st);
     else
       launch_accumulate<Fq2>(points, vals_sorted_, bstart_, bend_, off_a_, nb, (uint32_t)prm_.S, part_a_,
                              max_tasks_now, st);
+    if (slot >= 0) {
+      HIPX(hipEventRecord(ev_[slot][1], st));
+      // valid entries = start of the INVALID bucket (total if there is none); tasks = off_a[nb]
+      h_total_[slot] = total;
+      HIPX(hipMemcpyAsync(&h_counts_[3 * slot], &bstart_[nb], 4, hipMemcpyDeviceToHost, st));
+      HIPX(hipMemcpyAsync(&h_counts_[3 * slot + 1], &bend_[nb], 4, hipMemcpyDeviceToHost, st));
+      HIPX(hipMemcpyAsync(&h_counts_[3 * slot + 2], &off_a_[nb], 4, hipMemcpyDeviceToHost, st));
+    }
     // segmented merge levels: part_a/off_a -> part_b/off_b -> ...
     uint32_t *pin = part_a_, *pout = part_b_, *oin = off_a_, *oout = off_b_;
     size_t bound = max_tasks_now;

@@ -59,6 +59,19 @@ class MsmEngine {
   // synchronised: the caller orders/awaits the stream.
   void run(const uint32_t* points, const uint32_t* scalars, size_t n, uint32_t* d_out);
   size_t window_words() const { return (size_t)prm_.windows * 4 * fwords_; }
+
+  // Kernel instrumentation (HIP events on this engine's stream).  When enabled,
+  // every run() brackets the bucket-accumulate kernel with events and copies the
+  // number of nonzero digits (= mixed additions) to pinned memory.  collect()
+  // must be called after the stream is synchronised.
+  struct Stats {
+    double accumulate_ms = 0;  // summed over launches
+    uint64_t launches = 0;
+    uint64_t mixed_adds = 0;   // nonzero (point, window) digits processed
+    uint64_t tasks = 0;
+  };
+  void set_instrument(bool on) { instrument_ = on; }
+  void collect(Stats& s);
   const MsmParams& params() const { return prm_; }
   Curve curve() const { return curve_; }
   hipStream_t stream() const { return stream_; }
@@ -83,6 +96,13 @@ class MsmEngine {
   void* scan_tmp_ = nullptr;
   size_t scan_tmp_bytes_ = 0;
   int fwords_;  // words per field element (8 or 16)
+  // instrumentation
+  static constexpr int MAX_PENDING = 16;
+  bool instrument_ = false;
+  int pending_ = 0;
+  hipEvent_t ev_[MAX_PENDING][2];
+  uint32_t* h_counts_ = nullptr;  // pinned: [invalid-bucket start, end, tasks] per pending run
+  uint32_t h_total_[MAX_PENDING] = {};
 };
 
 }  // namespace zkp

@@ -298,6 +298,8 @@ class DevicePipeline {
                     (void*)col_[0], (void*)col_[1], (void*)val_[0], (void*)val_[1], (void*)wit_, (void*)abc_[0],
                     (void*)abc_[1], (void*)abc_[2], (void*)pscal_, (void*)dwin_})
       if (p) (void)hipFree(p);
+    for (uint32_t* p : slots_)
+      if (p) (void)hipFree(p);
     if (hwin_) (void)hipHostFree(hwin_);
     for (auto& e : ev_) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(s0_);
@@ -305,12 +307,17 @@ class DevicePipeline {
   }
 
   // enqueue witness upload + quotient (A4..A8); result scalars in pscal_
-  void enqueue_quotient(const WtnsView& w) {
-    const ZkeyHeader& h = hdr_;
+  // witness H2D into dst, bracketed by ev_[0]/ev_[1]
+  void upload(const WtnsView& w, uint32_t* dst) {
     HIPX(hipEventRecord(ev_[0], s0_));
-    HIPX(hipMemcpyAsync(wit_, w.values, (size_t)h.n_vars * 32, hipMemcpyHostToDevice, s0_));
+    HIPX(hipMemcpyAsync(dst, w.values, (size_t)hdr_.n_vars * 32, hipMemcpyHostToDevice, s0_));
     HIPX(hipEventRecord(ev_[1], s0_));
-    launch_build_abc(rowptr_[0], col_[0], val_[0], rowptr_[1], col_[1], val_[1], wit_, h.domain_size, abc_[0],
+  }
+
+  // quotient (rows A4..A8) from a device-resident witness; result scalars in pscal_
+  void enqueue_quotient(const uint32_t* d_wit) {
+    const ZkeyHeader& h = hdr_;
+    launch_build_abc(rowptr_[0], col_[0], val_[0], rowptr_[1], col_[1], val_[1], d_wit, h.domain_size, abc_[0],
                      abc_[1], abc_[2], s0_);
     HIPX(hipEventRecord(ev_[2], s0_));
     for (auto* b : abc_) ntt_->coset_extend(b);
@@ -318,10 +325,40 @@ class DevicePipeline {
     HIPX(hipEventRecord(ev_[3], s0_));
   }
 
+  // keep a witness resident in HBM slot `slot` (benchmarks: timing without PCIe)
+  void stage(int slot, const WtnsView& w) {
+    std::lock_guard<std::mutex> lk(mu_);
+    HIPX(hipSetDevice(dev_));
+    if (slot < 0 || slot > 4096) throw ZkpError(ZKP_ERR_INVALID_ARG, "bad staging slot");
+    if ((size_t)slot >= slots_.size()) slots_.resize(slot + 1, nullptr);
+    if (!slots_[slot]) HIPX(hipMalloc(&slots_[slot], (size_t)hdr_.n_vars * 32));
+    HIPX(hipMemcpyAsync(slots_[slot], w.values, (size_t)hdr_.n_vars * 32, hipMemcpyHostToDevice, s0_));
+    HIPX(hipStreamSynchronize(s0_));
+  }
+  const uint32_t* slot_ptr(int slot) const {
+    if (slot < 0 || (size_t)slot >= slots_.size() || !slots_[slot])
+      throw ZkpError(ZKP_ERR_INVALID_ARG, "staging slot is empty");
+    return slots_[slot];
+  }
+
+  void set_instrument(bool on) {
+    std::lock_guard<std::mutex> lk(mu_);
+    g1_->set_instrument(on);
+    g2_->set_instrument(on);
+    stats_g1_ = MsmEngine::Stats{};
+    stats_g2_ = MsmEngine::Stats{};
+  }
+  void stats(MsmEngine::Stats& g1, MsmEngine::Stats& g2) {
+    std::lock_guard<std::mutex> lk(mu_);
+    g1 = stats_g1_;
+    g2 = stats_g2_;
+  }
+
   void quotient(const WtnsView& w, uint8_t* out) {
     std::lock_guard<std::mutex> lk(mu_);
     HIPX(hipSetDevice(dev_));
-    enqueue_quotient(w);
+    upload(w, wit_);
+    enqueue_quotient(wit_);
     HIPX(hipMemcpyAsync(out, pscal_, (size_t)hdr_.domain_size * 32, hipMemcpyDeviceToHost, s0_));
     HIPX(hipStreamSynchronize(s0_));
   }
@@ -335,23 +372,40 @@ class DevicePipeline {
   MsmOut prove(const WtnsView& w) {
     std::lock_guard<std::mutex> lk(mu_);
     HIPX(hipSetDevice(dev_));
+    upload(w, wit_);
+    return prove_dev(wit_);
+  }
+
+  MsmOut prove_staged(int slot) {
+    std::lock_guard<std::mutex> lk(mu_);
+    HIPX(hipSetDevice(dev_));
+    const uint32_t* d = slot_ptr(slot);
+    HIPX(hipEventRecord(ev_[0], s0_));
+    HIPX(hipEventRecord(ev_[1], s0_));
+    return prove_dev(d);
+  }
+
+  // the whole device pipeline on a resident witness (caller holds mu_, ev_[0..1] recorded)
+  MsmOut prove_dev(const uint32_t* d_wit) {
     const ZkeyHeader& h = hdr_;
-    enqueue_quotient(w);
+    enqueue_quotient(d_wit);
     // G2 MSM (B2) on s1 as soon as the witness is resident
     HIPX(hipStreamWaitEvent(s1_, ev_[1], 0));
     HIPX(hipEventRecord(ev_[7], s1_));
-    g2_->run(pb2_, wit_, h.n_vars, dwin_ + 4 * win1_);
+    g2_->run(pb2_, d_wit, h.n_vars, dwin_ + 4 * win1_);
     HIPX(hipEventRecord(ev_[6], s1_));
     // G1 MSMs on s0 after the quotient
-    g1_->run(pa_, wit_, h.n_vars, dwin_);
-    g1_->run(pb1_, wit_, h.n_vars, dwin_ + win1_);
-    g1_->run(pc_, wit_ + (size_t)(h.n_public + 1) * 8, h.n_vars - h.n_public - 1, dwin_ + 2 * win1_);
+    g1_->run(pa_, d_wit, h.n_vars, dwin_);
+    g1_->run(pb1_, d_wit, h.n_vars, dwin_ + win1_);
+    g1_->run(pc_, d_wit + (size_t)(h.n_public + 1) * 8, h.n_vars - h.n_public - 1, dwin_ + 2 * win1_);
     g1_->run(ph_, pscal_, h.domain_size, dwin_ + 3 * win1_);
     HIPX(hipEventRecord(ev_[4], s0_));
     HIPX(hipStreamWaitEvent(s0_, ev_[6], 0));
     HIPX(hipMemcpyAsync(hwin_, dwin_, (4 * win1_ + win2_) * 4, hipMemcpyDeviceToHost, s0_));
     HIPX(hipEventRecord(ev_[5], s0_));
     HIPX(hipStreamSynchronize(s0_));
+    g1_->collect(stats_g1_);
+    g2_->collect(stats_g2_);
     MsmOut o;
     const int W1 = g1_->params().windows, c1 = g1_->params().c;
     const int W2 = g2_->params().windows, c2 = g2_->params().c;
@@ -386,6 +440,8 @@ class DevicePipeline {
   uint32_t* dwin_ = nullptr;
   uint32_t* hwin_ = nullptr;
   std::mutex mu_;
+  std::vector<uint32_t*> slots_;
+  MsmEngine::Stats stats_g1_, stats_g2_;
 };
 
 // ------------------------------------------------------------------ Prover
@@ -497,6 +553,53 @@ void Prover::timings(float* ms, int n) const {
   for (int i = 0; i < n && i < 7; ++i) ms[i] = last_ms_[i];
 }
 
+void Prover::stage(int dev, int slot, const uint8_t* wtns, size_t len) {
+  if (dev < 0 || dev >= (int)devs_.size()) throw ZkpError(ZKP_ERR_INVALID_ARG, "device index out of range");
+  WtnsView w = check_wtns(hdr_, wtns, len);
+  devs_[dev]->stage(slot, w);
+  std::lock_guard<std::mutex> lk(smu_);
+  if (staged_pub_.size() < devs_.size()) staged_pub_.resize(devs_.size());
+  auto& v = staged_pub_[dev];
+  if ((size_t)slot >= v.size()) v.resize(slot + 1);
+  v[slot].assign(w.values, w.values + (size_t)(hdr_.n_public + 1) * 32);
+}
+
+void Prover::prove_staged(int dev, int slot, const uint8_t* r32, const uint8_t* s32, zkp_proof* out) {
+  if (dev < 0 || dev >= (int)devs_.size()) throw ZkpError(ZKP_ERR_INVALID_ARG, "device index out of range");
+  auto t0 = std::chrono::steady_clock::now();
+  DevicePipeline::MsmOut m = devs_[dev]->prove_staged(slot);
+  auto t1 = std::chrono::steady_clock::now();
+  WtnsView w;
+  {
+    std::lock_guard<std::mutex> lk(smu_);
+    w.values = staged_pub_[dev][slot].data();
+    w.n_witness = hdr_.n_vars;
+  }
+  assemble(hdr_, m, w, r32, s32, out);
+  auto t2 = std::chrono::steady_clock::now();
+  std::lock_guard<std::mutex> lk(tmu_);
+  for (int i = 0; i < 5; ++i) last_ms_[i] = m.ms[i];
+  last_ms_[5] = std::chrono::duration<float, std::milli>(t2 - t1).count();
+  last_ms_[6] = std::chrono::duration<float, std::milli>(t2 - t0).count();
+}
+
+void Prover::set_instrument(bool on) {
+  for (auto& d : devs_) d->set_instrument(on);
+}
+
+void Prover::kernel_stats(double* out, int n) const {
+  MsmEngine::Stats a{}, b{};
+  for (auto& d : devs_) {
+    MsmEngine::Stats x, y;
+    d->stats(x, y);
+    a.accumulate_ms += x.accumulate_ms, a.launches += x.launches, a.mixed_adds += x.mixed_adds, a.tasks += x.tasks;
+    b.accumulate_ms += y.accumulate_ms, b.launches += y.launches, b.mixed_adds += y.mixed_adds, b.tasks += y.tasks;
+  }
+  const double v[8] = {a.accumulate_ms, (double)a.launches, (double)a.mixed_adds, (double)a.tasks,
+                       b.accumulate_ms, (double)b.launches, (double)b.mixed_adds, (double)b.tasks};
+  for (int i = 0; i < n && i < 8; ++i) out[i] = v[i];
+}
+
 // ------------------------------------------------------------------ kernel-level helpers
 
 void msm_points(int device, Curve curve, const uint8_t* points, const uint8_t* scalars, size_t n, uint8_t* out,
@@ -549,6 +652,116 @@ void msm_points(int device, Curve curve, const uint8_t* points, const uint8_t* s
   for (void* p : {(void*)dp, (void*)ds, (void*)dw})
     if (p) (void)hipFree(p);
   HIPX(hipStreamDestroy(st));
+}
+
+MsmBench bench_msm(int device, Curve curve, const uint8_t* points, const uint8_t* scalars, size_t n, int warmup,
+                   int iters, uint8_t* out, int* is_inf) {
+  if (n == 0 || iters <= 0) throw ZkpError(ZKP_ERR_INVALID_ARG, "bench_msm: n and iters must be > 0");
+  HIPX(hipSetDevice(device));
+  hipStream_t st;
+  HIPX(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  const size_t pbytes = n * (curve == Curve::G1 ? 64 : 128);
+  uint32_t *dp = nullptr, *ds = nullptr, *dw = nullptr;
+  hipEvent_t e0, e1;
+  HIPX(hipEventCreate(&e0));
+  HIPX(hipEventCreate(&e1));
+  MsmBench r;
+  try {
+    MsmEngine eng(curve, n, st);
+    HIPX(hipMalloc(&dp, pbytes));
+    HIPX(hipMalloc(&ds, n * 32));
+    HIPX(hipMalloc(&dw, eng.window_words() * 4));
+    HIPX(hipMemcpyAsync(dp, points, pbytes, hipMemcpyHostToDevice, st));
+    HIPX(hipMemcpyAsync(ds, scalars, n * 32, hipMemcpyHostToDevice, st));
+    launch_convert_fq_zkey(dp, n * (curve == Curve::G1 ? 2 : 4), st);
+    for (int i = 0; i < warmup; ++i) eng.run(dp, ds, n, dw);
+    HIPX(hipStreamSynchronize(st));
+    // pass 1: whole-pipeline time, nothing but the MSM launches between the events
+    HIPX(hipEventRecord(e0, st));
+    for (int i = 0; i < iters; ++i) eng.run(dp, ds, n, dw);
+    HIPX(hipEventRecord(e1, st));
+    HIPX(hipEventSynchronize(e1));
+    float ms = 0;
+    HIPX(hipEventElapsedTime(&ms, e0, e1));
+    r.ms_per_msm = ms / iters;
+    // pass 2: per-launch events around the bucket-accumulate kernel
+    eng.set_instrument(true);
+    MsmEngine::Stats s;
+    for (int i = 0; i < std::min(iters, 8); ++i) eng.run(dp, ds, n, dw);
+    HIPX(hipStreamSynchronize(st));
+    eng.collect(s);
+    r.ms_accumulate = (float)(s.accumulate_ms / std::max<uint64_t>(1, s.launches));
+    r.mixed_adds = s.mixed_adds / std::max<uint64_t>(1, s.launches);
+    r.tasks = s.tasks / std::max<uint64_t>(1, s.launches);
+    r.c = eng.params().c;
+    r.windows = eng.params().windows;
+    std::vector<uint32_t> hw(eng.window_words());
+    HIPX(hipMemcpyAsync(hw.data(), dw, hw.size() * 4, hipMemcpyDeviceToHost, st));
+    HIPX(hipStreamSynchronize(st));
+    if (out && is_inf) {
+      if (curve == Curve::G1) {
+        auto a = host::jac_to_aff(fold_windows<HFq>(hw.data(), r.windows, r.c));
+        *is_inf = a.inf;
+        std::memset(out, 0, 64);
+        if (!a.inf) put_fq(a.x, out), put_fq(a.y, out + 32);
+      } else {
+        auto a = host::jac_to_aff(fold_windows<HFq2>(hw.data(), r.windows, r.c));
+        *is_inf = a.inf;
+        std::memset(out, 0, 128);
+        if (!a.inf) put_fq(a.x.c0, out), put_fq(a.x.c1, out + 32), put_fq(a.y.c0, out + 64), put_fq(a.y.c1, out + 96);
+      }
+    }
+  } catch (...) {
+    for (void* p : {(void*)dp, (void*)ds, (void*)dw})
+      if (p) (void)hipFree(p);
+    (void)hipEventDestroy(e0), (void)hipEventDestroy(e1), (void)hipStreamDestroy(st);
+    throw;
+  }
+  for (void* p : {(void*)dp, (void*)ds, (void*)dw})
+    if (p) (void)hipFree(p);
+  (void)hipEventDestroy(e0), (void)hipEventDestroy(e1);
+  HIPX(hipStreamDestroy(st));
+  return r;
+}
+
+float bench_ntt(int device, int log_n, int warmup, int iters) {
+  if (iters <= 0) throw ZkpError(ZKP_ERR_INVALID_ARG, "bench_ntt: iters must be > 0");
+  HIPX(hipSetDevice(device));
+  hipStream_t st;
+  HIPX(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  const size_t n = size_t(1) << log_n;
+  uint32_t* d = nullptr;
+  hipEvent_t e0, e1;
+  HIPX(hipEventCreate(&e0));
+  HIPX(hipEventCreate(&e1));
+  float ms = 0;
+  try {
+    NttEngine eng(log_n, st);
+    HIPX(hipMalloc(&d, n * 32));
+    HIPX(hipMemsetAsync(d, 0x11, n * 32, st));  // any values < 2^256 with top bits clear work
+    std::vector<uint32_t> seed(n * 8);
+    uint64_t x = 0x5A4B5032;
+    for (auto& v : seed) {  // uniform-ish Fr-sized values
+      x = x * 6364136223846793005ull + 1442695040888963407ull;
+      v = (uint32_t)(x >> 32);
+    }
+    for (size_t i = 0; i < n; ++i) seed[i * 8 + 7] &= 0x0fffffffu;
+    HIPX(hipMemcpyAsync(d, seed.data(), n * 32, hipMemcpyHostToDevice, st));
+    for (int i = 0; i < warmup; ++i) eng.coset_extend(d);
+    HIPX(hipEventRecord(e0, st));
+    for (int i = 0; i < iters; ++i) eng.coset_extend(d);
+    HIPX(hipEventRecord(e1, st));
+    HIPX(hipEventSynchronize(e1));
+    HIPX(hipEventElapsedTime(&ms, e0, e1));
+  } catch (...) {
+    if (d) (void)hipFree(d);
+    (void)hipEventDestroy(e0), (void)hipEventDestroy(e1), (void)hipStreamDestroy(st);
+    throw;
+  }
+  HIPX(hipFree(d));
+  (void)hipEventDestroy(e0), (void)hipEventDestroy(e1);
+  HIPX(hipStreamDestroy(st));
+  return ms / iters;
 }
 
 void ntt_fr(int device, uint8_t* data, size_t n, int mode) {

@@ -71,10 +71,19 @@ class Prover {
                    const uint8_t* const* s32s, zkp_proof* outs);
   void quotient(const uint8_t* wtns, size_t len, uint8_t* out);
   void timings(float* ms, int n) const;
+  // HBM-resident witnesses (benchmarks time the proof without the PCIe copy)
+  void stage(int dev, int slot, const uint8_t* wtns, size_t len);
+  void prove_staged(int dev, int slot, const uint8_t* r32, const uint8_t* s32, zkp_proof* out);
+  // per-kernel HIP-event statistics of the bucket-accumulate kernels
+  void set_instrument(bool on);
+  void kernel_stats(double* out, int n) const;
+  int device_count() const { return (int)devs_.size(); }
 
  private:
   ZkeyHeader hdr_;
   std::vector<std::unique_ptr<DevicePipeline>> devs_;
+  std::vector<std::vector<std::vector<uint8_t>>> staged_pub_;  // [dev][slot] -> first (nPub+1)*32 witness bytes
+  mutable std::mutex smu_;
   std::atomic<unsigned> rr_{0};
   mutable std::mutex tmu_;
   float last_ms_[7] = {0, 0, 0, 0, 0, 0, 0};
@@ -85,5 +94,16 @@ class Prover {
 void msm_points(int device, Curve curve, const uint8_t* points, const uint8_t* scalars, size_t n, uint8_t* out,
                 int* is_inf);
 void ntt_fr(int device, uint8_t* data, size_t n, int mode);
+// device-resident kernel benchmarks (HIP events on the engine stream)
+struct MsmBench {
+  float ms_per_msm = 0;         // whole MSM pipeline
+  float ms_accumulate = 0;      // bucket-accumulate kernel, per launch
+  uint64_t mixed_adds = 0;      // per launch
+  uint64_t tasks = 0;           // per launch
+  int c = 0, windows = 0;
+};
+MsmBench bench_msm(int device, Curve curve, const uint8_t* points, const uint8_t* scalars, size_t n, int warmup,
+                   int iters, uint8_t* out, int* is_inf);
+float bench_ntt(int device, int log_n, int warmup, int iters);  // ms per coset_extend (iNTT + coset + NTT)
 
 }  // namespace zkp

@@ -91,9 +91,19 @@ def load_library(path: str = LIB_PATH):
         lib.zkp_msm_g2.argtypes = [ctypes.c_int, u8p, u8p, sz, u8p, ctypes.POINTER(ctypes.c_int)]
         lib.zkp_ntt_fr.argtypes = [ctypes.c_int, u8p, sz, ctypes.c_int]
         lib.zkp_quotient.argtypes = [P, u8p, sz, u8p]
+        lib.zkp_witness_stage.argtypes = [P, ctypes.c_int, ctypes.c_int, u8p, sz]
+        lib.zkp_prove_staged.argtypes = [P, ctypes.c_int, ctypes.c_int, u8p, u8p, ctypes.POINTER(_Proof)]
+        lib.zkp_prover_instrument.argtypes = [P, ctypes.c_int]
+        lib.zkp_prover_kernel_stats.argtypes = [P, ctypes.POINTER(ctypes.c_double), ctypes.c_int]
+        lib.zkp_bench_msm.argtypes = [ctypes.c_int, ctypes.c_int, u8p, u8p, sz, ctypes.c_int, ctypes.c_int,
+                                      ctypes.POINTER(ctypes.c_double), u8p, ctypes.POINTER(ctypes.c_int)]
+        lib.zkp_bench_ntt.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                      ctypes.POINTER(ctypes.c_double)]
         for name in ("zkp_prover_load_mem", "zkp_prover_load_file", "zkp_prover_info", "zkp_prove",
                      "zkp_prove_batch", "zkp_prove_files", "zkp_proof_json", "zkp_public_json",
-                     "zkp_prover_timings", "zkp_msm_g1", "zkp_msm_g2", "zkp_ntt_fr", "zkp_quotient"):
+                     "zkp_prover_timings", "zkp_msm_g1", "zkp_msm_g2", "zkp_ntt_fr", "zkp_quotient",
+                     "zkp_witness_stage", "zkp_prove_staged", "zkp_prover_instrument", "zkp_prover_kernel_stats",
+                     "zkp_bench_msm", "zkp_bench_ntt"):
             getattr(lib, name).restype = ctypes.c_int
         _lib = lib
         return lib
@@ -127,7 +137,10 @@ class Prover:
         devs = list(devices or [])
         darr = (ctypes.c_int * max(1, len(devs)))(*devs) if devs else None
         dptr = ctypes.cast(darr, ctypes.POINTER(ctypes.c_int)) if darr is not None else None
-        if isinstance(zkey, (bytes, bytearray, memoryview)):
+        if hasattr(zkey, "ptr") and hasattr(zkey, "len"):  # library-owned buffer (e.g. synth.ZkeyBuffer)
+            _check(lib.zkp_prover_load_mem(ctypes.cast(zkey.ptr, ctypes.POINTER(ctypes.c_uint8)), zkey.len, dptr,
+                                           len(devs), ctypes.byref(h)))
+        elif isinstance(zkey, (bytes, bytearray, memoryview)):
             p, keep = _buf(bytes(zkey))
             _check(lib.zkp_prover_load_mem(p, len(zkey), dptr, len(devs), ctypes.byref(h)))
             del keep
@@ -224,6 +237,27 @@ class Prover:
         _check(lib.zkp_prover_timings(self._h, ms, 7))
         keys = ["wtns_h2d", "build_abc", "ntt_quotient", "msm_g1", "msm_g2", "host_assembly", "total_wall"]
         return dict(zip(keys, list(ms)))
+
+    def stage(self, wtns: bytes, slot: int, dev_index: int = 0):
+        wp, wk = _buf(wtns)
+        _check(load_library().zkp_witness_stage(self._h, dev_index, slot, wp, len(wtns)))
+
+    def prove_staged_raw(self, slot: int, r=None, s=None, dev_index: int = 0):
+        rp, rk = self._scalar(r)
+        sp, sk = self._scalar(s)
+        pr, pub = self._new_proof()
+        _check(load_library().zkp_prove_staged(self._h, dev_index, slot, rp, sp, ctypes.byref(pr)))
+        return _unpack_proof(pr, pub)
+
+    def instrument(self, on: bool = True):
+        _check(load_library().zkp_prover_instrument(self._h, 1 if on else 0))
+
+    def kernel_stats(self):
+        out = (ctypes.c_double * 8)()
+        _check(load_library().zkp_prover_kernel_stats(self._h, out, 8))
+        v = list(out)
+        return {"g1": {"accumulate_ms": v[0], "launches": int(v[1]), "mixed_adds": int(v[2]), "tasks": int(v[3])},
+                "g2": {"accumulate_ms": v[4], "launches": int(v[5]), "mixed_adds": int(v[6]), "tasks": int(v[7])}}
 
     def prove_files(self, wtns_path, proof_path, public_path):
         _check(load_library().zkp_prove_files(self._h, os.fsencode(wtns_path), os.fsencode(proof_path),
@@ -325,3 +359,34 @@ def ntt_fr(values, mode: int, device: int = 0):
     _check(lib.zkp_ntt_fr(device, ctypes.cast(arr, ctypes.POINTER(ctypes.c_uint8)), len(values), mode))
     out = bytes(arr)
     return [_le(out[32 * i:32 * i + 32]) for i in range(len(values))]
+
+
+def bench_msm(points_lem: bytes, scalars_le: bytes, g2: bool = False, warmup: int = 2, iters: int = 10,
+              device: int = 0):
+    """Device-resident MSM timing (HIP events on the engine stream).  Returns (stats dict, result)."""
+    lib = load_library()
+    n = len(scalars_le) // 32
+    pp, pk = _buf(points_lem)
+    sp, sk = _buf(scalars_le)
+    st = (ctypes.c_double * 6)()
+    out = (ctypes.c_uint8 * 128)()
+    inf = ctypes.c_int()
+    _check(lib.zkp_bench_msm(device, 1 if g2 else 0, pp, sp, n, warmup, iters, st,
+                             ctypes.cast(out, ctypes.POINTER(ctypes.c_uint8)), ctypes.byref(inf)))
+    raw = bytes(out)
+    if inf.value:
+        res = None
+    elif g2:
+        v = [_le(raw[32 * i:32 * i + 32]) for i in range(4)]
+        res = ((v[0], v[1]), (v[2], v[3]))
+    else:
+        res = (_le(raw[:32]), _le(raw[32:64]))
+    stats = {"ms_per_msm": st[0], "ms_accumulate": st[1], "mixed_adds": int(st[2]), "tasks": int(st[3]),
+             "c": int(st[4]), "windows": int(st[5])}
+    return stats, res
+
+
+def bench_ntt(log_n: int, warmup: int = 2, iters: int = 10, device: int = 0) -> float:
+    ms = ctypes.c_double()
+    _check(load_library().zkp_bench_ntt(device, log_n, warmup, iters, ctypes.byref(ms)))
+    return ms.value
