@@ -1,0 +1,74 @@
+'use strict';
+/*
+ * Drop-in for snarkjs' `groth16.prove(zkeyFileName, witnessFileName, logger)`
+ * (snarkjs@0.4.22, reference package-lock.json:3884-3896; callers
+ * app/src/helpers/zkp.ts:94 via fullProve, dizkus-scripts/5_gen_proof.sh:8 via the CLI).
+ *
+ * Same arguments (a path or a fastfile memory descriptor {type:"mem", data}), same
+ * Promise<{proof, publicSignals}> result with decimal strings and snarkjs' key order,
+ * same Error messages (from the C ABI).  The zkey is loaded once per process and stays
+ * resident in HBM (snarkjs re-reads it on every call).  There is no CPU fallback: if
+ * the native addon or libzkp_amd.so is missing, require() throws.
+ */
+const fs = require('fs');
+const path = require('path');
+const addon = require(path.join(__dirname, 'build', 'zkp_napi.node'));
+
+const provers = new Map();  // zkey path -> handle
+
+function readInput(x) {
+  if (x && typeof x === 'object' && x.type === 'mem') return Buffer.from(x.data.buffer ? x.data : Buffer.from(x.data));
+  if (Buffer.isBuffer(x)) return x;
+  return fs.readFileSync(x);
+}
+
+function proverFor(zkey, devices) {
+  if (typeof zkey === 'string') {
+    let h = provers.get(zkey);
+    if (!h) {
+      h = addon.loadProver(zkey, devices);
+      provers.set(zkey, h);
+    }
+    return h;
+  }
+  return addon.loadProver(readInput(zkey), devices);  // memory zkey: caller-owned lifetime
+}
+
+function toBuf32(v) {
+  if (v === undefined || v === null) return undefined;
+  if (Buffer.isBuffer(v)) return v;
+  let x = BigInt(v);
+  const b = Buffer.alloc(32);
+  for (let i = 0; i < 32; ++i) { b[i] = Number(x & 0xffn); x >>= 8n; }
+  return b;
+}
+
+/**
+ * @param zkeyFileName  path | {type:"mem", data}
+ * @param witnessFileName path | {type:"mem", data}
+ * @param logger        optional snarkjs-style logger ({debug, info})
+ * @param opts          {devices?: number[], r?: bigint|string, s?: bigint|string}  (r/s: tests only)
+ */
+async function prove(zkeyFileName, witnessFileName, logger, opts) {
+  opts = opts || {};
+  const h = proverFor(zkeyFileName, opts.devices);
+  const wtns = readInput(witnessFileName);
+  if (logger && logger.debug) logger.debug('zkp_amd: proving on MI355X');
+  const r = await addon.prove(h, wtns, toBuf32(opts.r), toBuf32(opts.s));
+  const proof = {
+    pi_a: [r.piA[0], r.piA[1], '1'],
+    pi_b: [[r.piB[0][0], r.piB[0][1]], [r.piB[1][0], r.piB[1][1]], ['1', '0']],
+    pi_c: [r.piC[0], r.piC[1], '1'],
+    protocol: 'groth16',
+    curve: 'bn128',
+  };
+  if (typeof zkeyFileName !== 'string') addon.freeProver(h);
+  return { proof, publicSignals: r.publicSignals };
+}
+
+function release() {
+  for (const h of provers.values()) addon.freeProver(h);
+  provers.clear();
+}
+
+module.exports = { groth16: { prove }, prove, release, version: addon.version };

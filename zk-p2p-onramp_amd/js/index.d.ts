@@ -1,0 +1,20 @@
+// Type declarations for the zkp_amd Node host layer (no tsc in the build image; this
+// documents the contract a TypeScript caller such as app/src/helpers/zkp.ts sees).
+export type Input = string | { type: 'mem'; data: Uint8Array };
+export interface Proof {
+  pi_a: [string, string, '1'];
+  pi_b: [[string, string], [string, string], ['1', '0']];
+  pi_c: [string, string, '1'];
+  protocol: 'groth16';
+  curve: 'bn128';
+}
+export interface ProveOptions { devices?: number[]; r?: bigint | string; s?: bigint | string }
+export interface Logger { debug?(msg: string): void; info?(msg: string): void }
+export declare const groth16: {
+  prove(zkeyFileName: Input, witnessFileName: Input, logger?: Logger, opts?: ProveOptions):
+    Promise<{ proof: Proof; publicSignals: string[] }>;
+};
+export declare function prove(zkey: Input, wtns: Input, logger?: Logger, opts?: ProveOptions):
+  Promise<{ proof: Proof; publicSignals: string[] }>;
+export declare function release(): void;
+export declare function version(): string;
