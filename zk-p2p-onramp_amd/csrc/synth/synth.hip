@@ -189,9 +189,9 @@ __global__ __launch_bounds__(256) void k_fixed_base(const uint32_t* __restrict__
     const uint32_t d = (s[w >> 3] >> ((w & 7) * 4)) & 15u;
     if (d) xyzz_add_aff(acc, load_aff<F>(table, (size_t)w * 15 + d - 1));
   }
-  uint32_t* o = out + i * 4 * FW;
+  uint32_t* o = out + i * 2 * FW;  // affine (x, y)
   if (xyzz_is_inf(acc)) {
-    for (int k = 0; k < 4 * FW; ++k) o[k] = 0;
+    for (int k = 0; k < 2 * FW; ++k) o[k] = 0;
     return;
   }
   const Fq k256 = load_fe<FqCfg>(k256w);
