@@ -46,7 +46,7 @@ def load_peak():
     p = os.path.join(ROOT, "profiles", "ubench_r01.json")
     try:
         with open(p) as f:
-            return json.load(f)["v_mad_u64_u32_tops"], p
+            return json.load(f)["v_mad_u64_u32_tops"], os.path.relpath(p, ROOT)
     except Exception:
         return None, None
 

@@ -87,8 +87,9 @@ zkp_status zkp_proof_json(const zkp_proof* proof, char* buf, size_t cap, size_t*
 zkp_status zkp_public_json(const zkp_proof* proof, char* buf, size_t cap, size_t* needed);
 
 /* Per-stage device timings (ms) of the last zkp_prove on this handle:
- * [0] wtns H2D, [1] buildABC, [2] NTT/quotient, [3] MSM G1 (A,B1,C,H), [4] MSM G2 (B2),
- * [5] host assembly, [6] total wall.  n = capacity of ms. */
+ * [0] wtns H2D, [1] buildABC, [2] NTT/quotient, [3] MSM G1 A,B1,C (own stream, overlaps
+ * [1]-[2]), [4] MSM G2 B2 (own stream), [5] host assembly, [6] total wall, [7] MSM G1 H.
+ * n = capacity of ms (entries beyond n are not written). */
 zkp_status zkp_prover_timings(const zkp_prover* p, float* ms, int n);
 
 void zkp_prover_free(zkp_prover* p);

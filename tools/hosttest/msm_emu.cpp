@@ -20,16 +20,30 @@ static host::Jac<HF> run(std::vector<uint32_t>& pts, std::vector<uint32_t>& sc, 
     store_fe(&pts[i * 8], x);
   }
   MsmParams prm = MsmParams::for_size(std::max<uint32_t>(n, 1));
-  const uint32_t W = prm.windows, half = 1u << (prm.c - 1), nb = W * half, total = n * W;
-  std::vector<uint32_t> keys(total), vals(total);
-  for (uint32_t i = 0; i < n; ++i) msmk::digits(i, sc.data(), n, prm.c, W, keys.data(), vals.data());
-  std::vector<uint32_t> idx(total);
+  const uint32_t W = prm.windows, half = 1u << (prm.c - 1), nb = W * half;
+  // compacted digit emission (window-major, point order) as k_digit_count/k_digit_write
+  std::vector<std::vector<std::pair<uint32_t, uint32_t>>> per(W);
+  for (uint32_t i = 0; i < n; ++i) {
+    uint32_t s[9];
+    msmk::load_scalar(sc.data(), i, s);
+    uint32_t carry = 0;
+    bool neg;
+    for (uint32_t w = 0; w < W; ++w) {
+      uint32_t key = msmk::digit_key(s, (int)w, prm.c, carry, neg, 0xffffffffu);
+      if (key != 0xffffffffu) per[w].push_back({key, i | (neg ? 0x80000000u : 0u)});
+    }
+  }
+  std::vector<uint32_t> ks, vs;
+  for (auto& v : per)
+    for (auto& e : v) ks.push_back(e.first), vs.push_back(e.second);
+  // stable sort on the bucket bits only (as the (c-1)-bit radix sort)
+  std::vector<uint32_t> idx(ks.size());
   std::iota(idx.begin(), idx.end(), 0);
-  std::stable_sort(idx.begin(), idx.end(), [&](uint32_t a, uint32_t b) { return keys[a] < keys[b]; });
-  std::vector<uint32_t> ks(total), vs(total);
-  for (uint32_t i = 0; i < total; ++i) { ks[i] = keys[idx[i]]; vs[i] = vals[idx[i]]; }
+  std::stable_sort(idx.begin(), idx.end(), [&](uint32_t a, uint32_t b) { return (ks[a] & (half - 1)) < (ks[b] & (half - 1)); });
+  { std::vector<uint32_t> k2(ks.size()), v2(ks.size()); for (size_t i = 0; i < idx.size(); ++i) { k2[i] = ks[idx[i]]; v2[i] = vs[idx[i]]; } ks.swap(k2); vs.swap(v2); }
+  const uint32_t total2 = (uint32_t)ks.size();
   std::vector<uint32_t> st(nb + 1, 0), en(nb + 1, 0), cnt(nb + 1), off(nb + 1);
-  for (uint32_t i = 0; i < total; ++i) msmk::bounds(i, ks.data(), total, st.data(), en.data());
+  for (uint32_t i = 0; i < total2; ++i) msmk::bounds(i, ks.data(), total2, st.data(), en.data());
   for (uint32_t b = 0; b <= nb; ++b) msmk::task_counts(b, st.data(), en.data(), nb, prm.S, cnt.data());
   uint32_t acc = 0;
   for (uint32_t b = 0; b <= nb; ++b) { off[b] = acc; acc += cnt[b]; }

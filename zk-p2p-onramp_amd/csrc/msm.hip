@@ -23,6 +23,70 @@ __global__ __launch_bounds__(TPB) void k_digits(const uint32_t* __restrict__ sca
                                                 uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
   msmk::digits(blockIdx.x * TPB + threadIdx.x, scalars, n, c, W, keys, vals);
 }
+constexpr int WAVES = TPB / 64;
+
+__device__ __forceinline__ uint32_t lane_rank(uint64_t m) {  // set bits of m below this lane
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// pass 1 of the compacted digit emission: nonzero digits per (window, block)
+__global__ __launch_bounds__(TPB) void k_digit_count(const uint32_t* __restrict__ scalars, uint32_t n, int c, int W,
+                                                     uint32_t* __restrict__ bcnt) {
+  __shared__ uint32_t cnt[32];
+  if (threadIdx.x < 32) cnt[threadIdx.x] = 0;
+  __syncthreads();
+  const uint32_t i = blockIdx.x * TPB + threadIdx.x;
+  const bool active = i < n;
+  uint32_t s[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  if (active) msmk::load_scalar(scalars, i, s);
+  const uint32_t invalid = 0xffffffffu;
+  uint32_t carry = 0;
+  bool neg;
+  for (int w = 0; w < W; ++w) {
+    const uint32_t key = msmk::digit_key(s, w, c, carry, neg, invalid);
+    const uint64_t m = __ballot(active && key != invalid);
+    if ((threadIdx.x & 63) == 0) atomicAdd(&cnt[w], (uint32_t)__popcll(m));
+  }
+  __syncthreads();
+  if (threadIdx.x < (unsigned)W) bcnt[(size_t)threadIdx.x * gridDim.x + blockIdx.x] = cnt[threadIdx.x];
+}
+
+// pass 2: write (key, point | sign) of every nonzero digit at
+//   boff[window][block] + (entries of earlier waves of the block) + (earlier lanes of the wave)
+// -> window-major, point order within a window (deterministic)
+__global__ __launch_bounds__(TPB) void k_digit_write(const uint32_t* __restrict__ scalars, uint32_t n, int c, int W,
+                                                     const uint32_t* __restrict__ boff, uint32_t* __restrict__ keys,
+                                                     uint32_t* __restrict__ vals) {
+  __shared__ uint32_t wcnt[32][WAVES];
+  const uint32_t i = blockIdx.x * TPB + threadIdx.x;
+  const int wave = threadIdx.x >> 6;
+  const bool active = i < n;
+  uint32_t s[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  if (active) msmk::load_scalar(scalars, i, s);
+  const uint32_t invalid = 0xffffffffu;
+  uint32_t carry = 0;
+  bool neg;
+  for (int w = 0; w < W; ++w) {
+    const uint32_t key = msmk::digit_key(s, w, c, carry, neg, invalid);
+    const uint64_t m = __ballot(active && key != invalid);
+    if ((threadIdx.x & 63) == 0) wcnt[w][wave] = (uint32_t)__popcll(m);
+  }
+  __syncthreads();
+  carry = 0;
+  for (int w = 0; w < W; ++w) {
+    const uint32_t key = msmk::digit_key(s, w, c, carry, neg, invalid);
+    const bool valid = active && key != invalid;
+    const uint64_t m = __ballot(valid);
+    if (valid) {
+      uint32_t base = boff[(size_t)w * gridDim.x + blockIdx.x];
+      for (int v = 0; v < wave; ++v) base += wcnt[w][v];
+      const uint32_t pos = base + lane_rank(m);
+      keys[pos] = key;
+      vals[pos] = i | (neg ? 0x80000000u : 0u);
+    }
+  }
+}
+
 __global__ __launch_bounds__(TPB) void k_bounds(const uint32_t* __restrict__ keys, uint32_t total,
                                                 uint32_t* __restrict__ start, uint32_t* __restrict__ end) {
   msmk::bounds(blockIdx.x * TPB + threadIdx.x, keys, total, start, end);
@@ -109,6 +173,10 @@ MsmEngine::MsmEngine(Curve curve, size_t max_n, hipStream_t stream)
   HIPX(hipMalloc(&cnt_, (nbuckets_ + 1) * 4));
   HIPX(hipMalloc(&off_a_, (nbuckets_ + 1) * 4));
   HIPX(hipMalloc(&off_b_, (nbuckets_ + 1) * 4));
+  const size_t ncnt = (size_t)prm_.windows * grid_for(max_n_) + 1;  // per (window, digit block) counts
+  HIPX(hipMalloc(&bcnt_, ncnt * 4));
+  HIPX(hipMalloc(&boff_, ncnt * 4));
+  HIPX(hipHostMalloc(&h_valid_, 4, hipHostMallocDefault));
   HIPX(hipMalloc(&part_a_, max_tasks_ * xyzz_words * 4));
   HIPX(hipMalloc(&part_b_, max_tasks_ * xyzz_words * 4));
   HIPX(hipMalloc(&buckets_, nbuckets_ * xyzz_words * 4));
@@ -122,7 +190,8 @@ MsmEngine::MsmEngine(Curve curve, size_t max_n, hipStream_t stream)
   HIPX(hipcub::DeviceRadixSort::SortPairs(nullptr, sort_tmp_bytes_, keys_, keys_sorted_, vals_, vals_sorted_,
                                           (int)max_entries_, 0, end_bit, stream_));
   HIPX(hipMalloc(&sort_tmp_, sort_tmp_bytes_));
-  HIPX(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_tmp_bytes_, cnt_, off_a_, (int)(nbuckets_ + 1), stream_));
+  HIPX(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_tmp_bytes_, cnt_, off_a_,
+                                        (int)std::max(nbuckets_ + 1, ncnt), stream_));
   HIPX(hipMalloc(&scan_tmp_, scan_tmp_bytes_));
   for (auto& e : ev_) {
     HIPX(hipEventCreate(&e[0]));
@@ -137,8 +206,7 @@ void MsmEngine::collect(Stats& s) {
     HIPX(hipEventElapsedTime(&ms, ev_[i][0], ev_[i][1]));
     s.accumulate_ms += ms;
     s.launches += 1;
-    const uint32_t inv_start = h_counts_[3 * i], inv_end = h_counts_[3 * i + 1];
-    s.mixed_adds += inv_end ? inv_start : h_total_[i];
+    s.mixed_adds += h_total_[i];
     s.tasks += h_counts_[3 * i + 2];
   }
   pending_ = 0;
@@ -150,9 +218,11 @@ MsmEngine::~MsmEngine() {
     (void)hipEventDestroy(e[1]);
   }
   if (h_counts_) (void)hipHostFree(h_counts_);
+  if (h_valid_) (void)hipHostFree(h_valid_);
   for (void* p : {(void*)keys_, (void*)vals_, (void*)keys_sorted_, (void*)vals_sorted_, (void*)bstart_, (void*)bend_,
                   (void*)cnt_, (void*)off_a_, (void*)off_b_, (void*)part_a_, (void*)part_b_, (void*)buckets_,
-                  (void*)lvl_s_[0], (void*)lvl_s_[1], (void*)lvl_t_[0], (void*)lvl_t_[1], sort_tmp_, scan_tmp_})
+                  (void*)lvl_s_[0], (void*)lvl_s_[1], (void*)lvl_t_[0], (void*)lvl_t_[1], sort_tmp_, scan_tmp_,
+                  (void*)bcnt_, (void*)boff_})
     if (p) (void)hipFree(p);
 }
 
@@ -167,14 +237,26 @@ void MsmEngine::run(const uint32_t* points, const uint32_t* scalars, size_t n, u
     // all windows = infinity
     HIPX(hipMemsetAsync(buckets_, 0, nbuckets_ * xyzz_bytes, st));
   } else {
-    const uint32_t total = (uint32_t)(n * W);
-    hipLaunchKernelGGL(k_digits, dim3(grid_for(n)), dim3(TPB), 0, st, scalars, (uint32_t)n, prm_.c, (int)W, keys_,
-                       vals_);
-    int end_bit = 1;
-    while ((size_t(1) << end_bit) <= nbuckets_) ++end_bit;
-    size_t tmp = sort_tmp_bytes_;
-    HIPX(hipcub::DeviceRadixSort::SortPairs(sort_tmp_, tmp, keys_, keys_sorted_, vals_, vals_sorted_, (int)total, 0,
-                                            end_bit, st));
+    // 1. digits, compacted: only nonzero digits, window-major, point order within a window
+    const uint32_t nblk = grid_for(n);
+    hipLaunchKernelGGL(k_digit_count, dim3(nblk), dim3(TPB), 0, st, scalars, (uint32_t)n, prm_.c, (int)W, bcnt_);
+    HIPX(hipMemsetAsync(bcnt_ + (size_t)W * nblk, 0, 4, st));
+    size_t stmp0 = scan_tmp_bytes_;
+    HIPX(hipcub::DeviceScan::ExclusiveSum(scan_tmp_, stmp0, bcnt_, boff_, (int)((size_t)W * nblk + 1), st));
+    hipLaunchKernelGGL(k_digit_write, dim3(nblk), dim3(TPB), 0, st, scalars, (uint32_t)n, prm_.c, (int)W, boff_,
+                       keys_, vals_);
+    HIPX(hipMemcpyAsync(h_valid_, boff_ + (size_t)W * nblk, 4, hipMemcpyDeviceToHost, st));
+    HIPX(hipStreamSynchronize(st));  // the sort needs the entry count on the host
+    const uint32_t total = *h_valid_;
+    last_valid_ = total;
+    if (total == 0) {
+      HIPX(hipMemsetAsync(buckets_, 0, nbuckets_ * xyzz_bytes, st));
+    } else {
+      // 2. stable LSD sort on the (c-1) bucket bits only: windows stay grouped, so equal
+      //    (window, bucket) keys end up contiguous after 2 radix passes instead of 3
+      size_t tmp = sort_tmp_bytes_;
+      HIPX(hipcub::DeviceRadixSort::SortPairs(sort_tmp_, tmp, keys_, keys_sorted_, vals_, vals_sorted_, (int)total,
+                                              0, prm_.c - 1, st));
     HIPX(hipMemsetAsync(bstart_, 0, (nbuckets_ + 1) * 4, st));
     HIPX(hipMemsetAsync(bend_, 0, (nbuckets_ + 1) * 4, st));
     hipLaunchKernelGGL(k_bounds, dim3(grid_for(total)), dim3(TPB), 0, st, keys_sorted_, total, bstart_, bend_);
@@ -193,10 +275,7 @@ void MsmEngine::run(const uint32_t* points, const uint32_t* scalars, size_t n, u
                              max_tasks_now, st);
     if (slot >= 0) {
       HIPX(hipEventRecord(ev_[slot][1], st));
-      // valid entries = start of the INVALID bucket (total if there is none); tasks = off_a[nb]
-      h_total_[slot] = total;
-      HIPX(hipMemcpyAsync(&h_counts_[3 * slot], &bstart_[nb], 4, hipMemcpyDeviceToHost, st));
-      HIPX(hipMemcpyAsync(&h_counts_[3 * slot + 1], &bend_[nb], 4, hipMemcpyDeviceToHost, st));
+      h_total_[slot] = total;  // every compacted entry is one mixed addition
       HIPX(hipMemcpyAsync(&h_counts_[3 * slot + 2], &off_a_[nb], 4, hipMemcpyDeviceToHost, st));
     }
     // segmented merge levels: part_a/off_a -> part_b/off_b -> ...
@@ -221,6 +300,7 @@ void MsmEngine::run(const uint32_t* points, const uint32_t* scalars, size_t n, u
       hipLaunchKernelGGL(k_merge_final<Fq>, dim3(grid_for(nbuckets_)), dim3(TPB), 0, st, pin, oin, nb, buckets_);
     else
       hipLaunchKernelGGL(k_merge_final<Fq2>, dim3(grid_for(nbuckets_)), dim3(TPB), 0, st, pin, oin, nb, buckets_);
+    }
   }
   // bucket reduction tree per window
   const uint32_t L = (uint32_t)prm_.L;

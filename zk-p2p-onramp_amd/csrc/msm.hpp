@@ -90,6 +90,9 @@ class MsmEngine {
   uint32_t *keys_ = nullptr, *vals_ = nullptr, *keys_sorted_ = nullptr, *vals_sorted_ = nullptr;
   uint32_t *bstart_ = nullptr, *bend_ = nullptr, *cnt_ = nullptr, *off_a_ = nullptr, *off_b_ = nullptr;
   uint32_t *part_a_ = nullptr, *part_b_ = nullptr, *buckets_ = nullptr;
+  uint32_t *bcnt_ = nullptr, *boff_ = nullptr;  // compacted digit emission: per (window, block) counts/offsets
+  uint32_t* h_valid_ = nullptr;                 // pinned: number of nonzero digits of the current run
+  uint32_t last_valid_ = 0;
   uint32_t *lvl_s_[2] = {nullptr, nullptr}, *lvl_t_[2] = {nullptr, nullptr};
   void* sort_tmp_ = nullptr;
   size_t sort_tmp_bytes_ = 0;

@@ -53,6 +53,32 @@ ZDEV void digits(uint32_t i, const uint32_t* __restrict__ scalars, uint32_t n, i
   }
 }
 
+// load scalar i as 9 words (word 8 = 0), reduced below r
+ZDEV void load_scalar(const uint32_t* __restrict__ scalars, uint32_t i, uint32_t (&s)[9]) {
+  const uint4* q = reinterpret_cast<const uint4*>(scalars + (size_t)i * 8);
+  uint4 a = q[0], b = q[1];
+  s[0] = a.x, s[1] = a.y, s[2] = a.z, s[3] = a.w, s[4] = b.x, s[5] = b.y, s[6] = b.z, s[7] = b.w, s[8] = 0u;
+  while (scalar_geq_r(s)) scalar_sub_r(s);
+}
+
+// signed c-bit digit of window w (windows visited in order, carry threaded through):
+// returns the key window*2^(c-1) + |d|-1, or `invalid` for a zero digit; neg = (d < 0)
+ZDEV uint32_t digit_key(const uint32_t (&s)[9], int w, int c, uint32_t& carry, bool& neg, uint32_t invalid) {
+  const uint32_t half = 1u << (c - 1), full = 1u << c;
+  const int bit = w * c, j = bit >> 5, sh = bit & 31;
+  const uint64_t v = (uint64_t)s[j] | ((uint64_t)s[j + 1] << 32);
+  const uint32_t raw = ((uint32_t)(v >> sh) & (full - 1)) + carry;
+  if (raw > half) {
+    carry = 1;
+    neg = true;
+    const uint32_t mag = full - raw;  // 0 when raw == 2^c: pure carry
+    return mag == 0 ? invalid : (uint32_t)w * half + mag - 1;
+  }
+  carry = 0;
+  neg = false;
+  return raw == 0 ? invalid : (uint32_t)w * half + raw - 1;
+}
+
 ZDEV void bounds(uint32_t i, const uint32_t* __restrict__ keys, uint32_t total, uint32_t* __restrict__ start,
                 uint32_t* __restrict__ end) {
   if (i >= total) return;

@@ -245,6 +245,7 @@ class DevicePipeline {
     HIPX(hipSetDevice(dev_));
     HIPX(hipStreamCreateWithFlags(&s0_, hipStreamNonBlocking));
     HIPX(hipStreamCreateWithFlags(&s1_, hipStreamNonBlocking));
+    HIPX(hipStreamCreateWithFlags(&s2_, hipStreamNonBlocking));
     for (auto& e : ev_) HIPX(hipEventCreate(&e));
     const ZkeyHeader& h = hdr_;
     const size_t nv = h.n_vars, nd = h.domain_size, nc = h.n_vars - h.n_public - 1;
@@ -280,19 +281,24 @@ class DevicePipeline {
     for (auto& b : abc_) HIPX(hipMalloc(&b, nd * 32));
     HIPX(hipMalloc(&pscal_, nd * 32));
     ntt_ = std::make_unique<NttEngine>((int)h.log_domain, s0_);
-    g1_ = std::make_unique<MsmEngine>(Curve::G1, std::max<size_t>(nv, nd), s0_);
+    // three engines on three streams: A/B1/C need only the witness and overlap the NTT;
+    // H follows the quotient on s0; the G2 MSM runs on s1
+    g1a_ = std::make_unique<MsmEngine>(Curve::G1, nv, s2_);
+    g1h_ = std::make_unique<MsmEngine>(Curve::G1, nd, s0_);
     g2_ = std::make_unique<MsmEngine>(Curve::G2, nv, s1_);
-    win1_ = g1_->window_words();
+    wina_ = g1a_->window_words();
+    winh_ = g1h_->window_words();
     win2_ = g2_->window_words();
-    HIPX(hipMalloc(&dwin_, (4 * win1_ + win2_) * 4));
-    HIPX(hipHostMalloc(&hwin_, (4 * win1_ + win2_) * 4, hipHostMallocDefault));
+    HIPX(hipMalloc(&dwin_, win_total() * 4));
+    HIPX(hipHostMalloc(&hwin_, win_total() * 4, hipHostMallocDefault));
     HIPX(hipStreamSynchronize(s0_));
   }
 
   ~DevicePipeline() {
     (void)hipSetDevice(dev_);
     ntt_.reset();
-    g1_.reset();
+    g1a_.reset();
+    g1h_.reset();
     g2_.reset();
     for (void* p : {(void*)pa_, (void*)pb1_, (void*)pb2_, (void*)pc_, (void*)ph_, (void*)rowptr_[0], (void*)rowptr_[1],
                     (void*)col_[0], (void*)col_[1], (void*)val_[0], (void*)val_[1], (void*)wit_, (void*)abc_[0],
@@ -304,6 +310,7 @@ class DevicePipeline {
     for (auto& e : ev_) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(s0_);
     (void)hipStreamDestroy(s1_);
+    (void)hipStreamDestroy(s2_);
   }
 
   // enqueue witness upload + quotient (A4..A8); result scalars in pscal_
@@ -343,7 +350,8 @@ class DevicePipeline {
 
   void set_instrument(bool on) {
     std::lock_guard<std::mutex> lk(mu_);
-    g1_->set_instrument(on);
+    g1a_->set_instrument(on);
+    g1h_->set_instrument(on);
     g2_->set_instrument(on);
     stats_g1_ = MsmEngine::Stats{};
     stats_g2_ = MsmEngine::Stats{};
@@ -366,7 +374,7 @@ class DevicePipeline {
   struct MsmOut {
     Jac<HFq> a, b1, c, h;
     Jac<HFq2> b2;
-    float ms[5];
+    float ms[6];
   };
 
   MsmOut prove(const WtnsView& w) {
@@ -388,45 +396,84 @@ class DevicePipeline {
   // the whole device pipeline on a resident witness (caller holds mu_, ev_[0..1] recorded)
   MsmOut prove_dev(const uint32_t* d_wit) {
     const ZkeyHeader& h = hdr_;
-    enqueue_quotient(d_wit);
-    // G2 MSM (B2) on s1 as soon as the witness is resident
+    // window-sum layout in dwin_: A | B1 | C (engine g1a) | H (g1h) | B2 (g2)
+    uint32_t* wa = dwin_;
+    uint32_t* wh = dwin_ + 3 * wina_;
+    uint32_t* wb2 = wh + winh_;
+    // s1: G2 MSM (B2) and s2: G1 MSMs A, B1, C — both need only the resident witness.
+    // MsmEngine::run blocks its host thread once (the sort needs the nonzero-digit count),
+    // so each stream is fed from its own host thread; otherwise the host would serialise
+    // the streams at those syncs.
     HIPX(hipStreamWaitEvent(s1_, ev_[1], 0));
-    HIPX(hipEventRecord(ev_[7], s1_));
-    g2_->run(pb2_, d_wit, h.n_vars, dwin_ + 4 * win1_);
-    HIPX(hipEventRecord(ev_[6], s1_));
-    // G1 MSMs on s0 after the quotient
-    g1_->run(pa_, d_wit, h.n_vars, dwin_);
-    g1_->run(pb1_, d_wit, h.n_vars, dwin_ + win1_);
-    g1_->run(pc_, d_wit + (size_t)(h.n_public + 1) * 8, h.n_vars - h.n_public - 1, dwin_ + 2 * win1_);
-    g1_->run(ph_, pscal_, h.domain_size, dwin_ + 3 * win1_);
+    HIPX(hipStreamWaitEvent(s2_, ev_[1], 0));
+    std::exception_ptr err[2];
+    std::thread t_g2([&] {
+      try {
+        HIPX(hipSetDevice(dev_));
+        HIPX(hipEventRecord(ev_[7], s1_));
+        g2_->run(pb2_, d_wit, h.n_vars, wb2);
+        HIPX(hipEventRecord(ev_[6], s1_));
+      } catch (...) {
+        err[0] = std::current_exception();
+      }
+    });
+    std::thread t_g1([&] {
+      try {
+        HIPX(hipSetDevice(dev_));
+        HIPX(hipEventRecord(ev_[9], s2_));
+        g1a_->run(pa_, d_wit, h.n_vars, wa);
+        g1a_->run(pb1_, d_wit, h.n_vars, wa + wina_);
+        g1a_->run(pc_, d_wit + (size_t)(h.n_public + 1) * 8, h.n_vars - h.n_public - 1, wa + 2 * wina_);
+        HIPX(hipEventRecord(ev_[8], s2_));
+      } catch (...) {
+        err[1] = std::current_exception();
+      }
+    });
+    // s0: quotient (buildABC, 3 coset NTTs, joinABC) then the H MSM
+    std::exception_ptr err0;
+    try {
+      enqueue_quotient(d_wit);
+      g1h_->run(ph_, pscal_, h.domain_size, wh);
+    } catch (...) {
+      err0 = std::current_exception();
+    }
+    t_g2.join();
+    t_g1.join();
+    if (err0) std::rethrow_exception(err0);
+    for (auto& e : err)
+      if (e) std::rethrow_exception(e);
     HIPX(hipEventRecord(ev_[4], s0_));
     HIPX(hipStreamWaitEvent(s0_, ev_[6], 0));
-    HIPX(hipMemcpyAsync(hwin_, dwin_, (4 * win1_ + win2_) * 4, hipMemcpyDeviceToHost, s0_));
+    HIPX(hipStreamWaitEvent(s0_, ev_[8], 0));
+    HIPX(hipMemcpyAsync(hwin_, dwin_, win_total() * 4, hipMemcpyDeviceToHost, s0_));
     HIPX(hipEventRecord(ev_[5], s0_));
     HIPX(hipStreamSynchronize(s0_));
-    g1_->collect(stats_g1_);
+    g1a_->collect(stats_g1_);
+    g1h_->collect(stats_g1_);
     g2_->collect(stats_g2_);
     MsmOut o;
-    const int W1 = g1_->params().windows, c1 = g1_->params().c;
+    const int Wa = g1a_->params().windows, ca = g1a_->params().c;
+    const int Wh = g1h_->params().windows, ch = g1h_->params().c;
     const int W2 = g2_->params().windows, c2 = g2_->params().c;
-    o.a = fold_windows<HFq>(hwin_, W1, c1);
-    o.b1 = fold_windows<HFq>(hwin_ + win1_, W1, c1);
-    o.c = fold_windows<HFq>(hwin_ + 2 * win1_, W1, c1);
-    o.h = fold_windows<HFq>(hwin_ + 3 * win1_, W1, c1);
-    o.b2 = fold_windows<HFq2>(hwin_ + 4 * win1_, W2, c2);
+    o.a = fold_windows<HFq>(hwin_, Wa, ca);
+    o.b1 = fold_windows<HFq>(hwin_ + wina_, Wa, ca);
+    o.c = fold_windows<HFq>(hwin_ + 2 * wina_, Wa, ca);
+    o.h = fold_windows<HFq>(hwin_ + 3 * wina_, Wh, ch);
+    o.b2 = fold_windows<HFq2>(hwin_ + 3 * wina_ + winh_, W2, c2);
     HIPX(hipEventElapsedTime(&o.ms[0], ev_[0], ev_[1]));  // wtns H2D
     HIPX(hipEventElapsedTime(&o.ms[1], ev_[1], ev_[2]));  // buildABC
     HIPX(hipEventElapsedTime(&o.ms[2], ev_[2], ev_[3]));  // NTT + join
-    HIPX(hipEventElapsedTime(&o.ms[3], ev_[3], ev_[4]));  // G1 MSMs
-    HIPX(hipEventElapsedTime(&o.ms[4], ev_[7], ev_[6]));  // G2 MSM
+    HIPX(hipEventElapsedTime(&o.ms[3], ev_[9], ev_[8]));  // G1 MSMs A, B1, C (s2)
+    HIPX(hipEventElapsedTime(&o.ms[4], ev_[7], ev_[6]));  // G2 MSM (s1)
+    HIPX(hipEventElapsedTime(&o.ms[5], ev_[3], ev_[4]));  // G1 MSM H (s0)
     return o;
   }
 
  private:
   int dev_;
   ZkeyHeader hdr_;
-  hipStream_t s0_ = nullptr, s1_ = nullptr;
-  hipEvent_t ev_[8];
+  hipStream_t s0_ = nullptr, s1_ = nullptr, s2_ = nullptr;
+  hipEvent_t ev_[12];
   uint32_t *pa_ = nullptr, *pb1_ = nullptr, *pb2_ = nullptr, *pc_ = nullptr, *ph_ = nullptr;
   uint32_t* rowptr_[2] = {nullptr, nullptr};
   uint32_t* col_[2] = {nullptr, nullptr};
@@ -435,8 +482,9 @@ class DevicePipeline {
   uint32_t* abc_[3] = {nullptr, nullptr, nullptr};
   uint32_t* pscal_ = nullptr;
   std::unique_ptr<NttEngine> ntt_;
-  std::unique_ptr<MsmEngine> g1_, g2_;
-  size_t win1_ = 0, win2_ = 0;
+  std::unique_ptr<MsmEngine> g1a_, g1h_, g2_;
+  size_t wina_ = 0, winh_ = 0, win2_ = 0;
+  size_t win_total() const { return 3 * wina_ + winh_ + win2_; }
   uint32_t* dwin_ = nullptr;
   uint32_t* hwin_ = nullptr;
   std::mutex mu_;
@@ -513,6 +561,7 @@ void Prover::prove(const uint8_t* wtns, size_t len, const uint8_t* r32, const ui
   auto t2 = std::chrono::steady_clock::now();
   std::lock_guard<std::mutex> lk(tmu_);
   for (int i = 0; i < 5; ++i) last_ms_[i] = m.ms[i];
+  last_ms_[7] = m.ms[5];
   last_ms_[5] = std::chrono::duration<float, std::milli>(t2 - t1).count();
   last_ms_[6] = std::chrono::duration<float, std::milli>(t2 - t0).count();
 }
@@ -550,7 +599,7 @@ void Prover::quotient(const uint8_t* wtns, size_t len, uint8_t* out) {
 
 void Prover::timings(float* ms, int n) const {
   std::lock_guard<std::mutex> lk(tmu_);
-  for (int i = 0; i < n && i < 7; ++i) ms[i] = last_ms_[i];
+  for (int i = 0; i < n && i < 8; ++i) ms[i] = last_ms_[i];
 }
 
 void Prover::stage(int dev, int slot, const uint8_t* wtns, size_t len) {
@@ -579,6 +628,7 @@ void Prover::prove_staged(int dev, int slot, const uint8_t* r32, const uint8_t* 
   auto t2 = std::chrono::steady_clock::now();
   std::lock_guard<std::mutex> lk(tmu_);
   for (int i = 0; i < 5; ++i) last_ms_[i] = m.ms[i];
+  last_ms_[7] = m.ms[5];
   last_ms_[5] = std::chrono::duration<float, std::milli>(t2 - t1).count();
   last_ms_[6] = std::chrono::duration<float, std::milli>(t2 - t0).count();
 }

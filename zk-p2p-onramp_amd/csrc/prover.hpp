@@ -86,7 +86,7 @@ class Prover {
   mutable std::mutex smu_;
   std::atomic<unsigned> rr_{0};
   mutable std::mutex tmu_;
-  float last_ms_[7] = {0, 0, 0, 0, 0, 0, 0};
+  float last_ms_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   friend class DevicePipeline;
 };
 

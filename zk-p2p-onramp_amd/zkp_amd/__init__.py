@@ -233,9 +233,10 @@ class Prover:
 
     def timings(self):
         lib = load_library()
-        ms = (ctypes.c_float * 7)()
-        _check(lib.zkp_prover_timings(self._h, ms, 7))
-        keys = ["wtns_h2d", "build_abc", "ntt_quotient", "msm_g1", "msm_g2", "host_assembly", "total_wall"]
+        ms = (ctypes.c_float * 8)()
+        _check(lib.zkp_prover_timings(self._h, ms, 8))
+        keys = ["wtns_h2d", "build_abc", "ntt_quotient", "msm_g1_abc", "msm_g2", "host_assembly", "total_wall",
+                "msm_g1_h"]
         return dict(zip(keys, list(ms)))
 
     def stage(self, wtns: bytes, slot: int, dev_index: int = 0):
