@@ -50,8 +50,21 @@ static host::Jac<HF> run(std::vector<uint32_t>& pts, std::vector<uint32_t>& sc, 
   const uint32_t ntask = off[nb];
   std::vector<uint32_t> part((size_t)(ntask + 1) * 4 * FW);
   for (uint32_t t = 0; t < ntask; ++t) msmk::accumulate<F>(t, pts.data(), vs.data(), st.data(), en.data(), off.data(), nb, prm.S, part.data());
+  // heavy-bucket merge levels (as MsmEngine::run)
+  int levels = 0;
+  for (size_t m = (n + prm.S - 1) / prm.S; m > (size_t)prm.S2; m = (m + prm.S2 - 1) / prm.S2) ++levels;
+  std::vector<uint32_t> part1(part.size()), hcnt(nb + 1), hoff(nb + 1);
+  for (int lv = 0; lv < levels; ++lv) {
+    for (uint32_t b = 0; b <= nb; ++b) msmk::heavy_counts(b, off.data(), nb, prm.S2, lv, hcnt.data());
+    uint32_t a2 = 0;
+    for (uint32_t b = 0; b <= nb; ++b) { hoff[b] = a2; a2 += hcnt[b]; }
+    const uint32_t* src = (lv & 1) ? part1.data() : part.data();
+    uint32_t* dst = (lv & 1) ? part.data() : part1.data();
+    for (uint32_t t = 0; t < hoff[nb]; ++t) msmk::merge_heavy<F>(t, src, off.data(), hoff.data(), nb, prm.S2, lv, dst);
+  }
   std::vector<uint32_t> buckets((size_t)nb * 4 * FW);
-  for (uint32_t b = 0; b < nb; ++b) msmk::merge_final<F>(b, part.data(), off.data(), nb, buckets.data());
+  for (uint32_t b = 0; b < nb; ++b)
+    msmk::merge_final<F>(b, part.data(), part1.data(), off.data(), nb, prm.S2, levels, buckets.data());
   uint32_t nodes = (half + prm.L - 1) / prm.L;
   std::vector<uint32_t> s0((size_t)W * nodes * 4 * FW), t0(s0.size()), s1(s0.size()), t1(s0.size());
   for (uint32_t id = 0; id < W * nodes; ++id) msmk::reduce_first<F>(id, buckets.data(), W, half, prm.L, s0.data(), t0.data());

@@ -96,9 +96,9 @@ __global__ __launch_bounds__(TPB) void k_task_counts(const uint32_t* __restrict_
                                                      uint32_t* __restrict__ cnt) {
   msmk::task_counts(blockIdx.x * TPB + threadIdx.x, start, end, nb, S, cnt);
 }
-__global__ __launch_bounds__(TPB) void k_seg_counts(const uint32_t* __restrict__ off, uint32_t nb, uint32_t S2,
-                                                    uint32_t* __restrict__ cnt) {
-  msmk::seg_counts(blockIdx.x * TPB + threadIdx.x, off, nb, S2, cnt);
+__global__ __launch_bounds__(TPB) void k_heavy_counts(const uint32_t* __restrict__ off, uint32_t nb, uint32_t S2,
+                                                      int lvl, uint32_t* __restrict__ cnt) {
+  msmk::heavy_counts(blockIdx.x * TPB + threadIdx.x, off, nb, S2, lvl, cnt);
 }
 template <class F>
 __global__ __launch_bounds__(TPB) void k_accumulate(const uint32_t* __restrict__ points,
@@ -110,16 +110,18 @@ __global__ __launch_bounds__(TPB) void k_accumulate(const uint32_t* __restrict__
   msmk::accumulate<F>(blockIdx.x * TPB + threadIdx.x, points, vals, start, end, off, nb, S, out);
 }
 template <class F>
-__global__ __launch_bounds__(TPB) void k_merge(const uint32_t* __restrict__ in, const uint32_t* __restrict__ in_off,
-                                               const uint32_t* __restrict__ out_off, uint32_t nb, uint32_t S2,
-                                               uint32_t* __restrict__ out) {
-  msmk::merge<F>(blockIdx.x * TPB + threadIdx.x, in, in_off, out_off, nb, S2, out);
+__global__ __launch_bounds__(TPB) void k_merge_heavy(const uint32_t* __restrict__ src,
+                                                     const uint32_t* __restrict__ off,
+                                                     const uint32_t* __restrict__ hoff, uint32_t nb, uint32_t S2,
+                                                     int lvl, uint32_t* __restrict__ dst) {
+  msmk::merge_heavy<F>(blockIdx.x * TPB + threadIdx.x, src, off, hoff, nb, S2, lvl, dst);
 }
 template <class F>
-__global__ __launch_bounds__(TPB) void k_merge_final(const uint32_t* __restrict__ in,
-                                                     const uint32_t* __restrict__ in_off, uint32_t nb,
-                                                     uint32_t* __restrict__ buckets) {
-  msmk::merge_final<F>(blockIdx.x * TPB + threadIdx.x, in, in_off, nb, buckets);
+__global__ __launch_bounds__(TPB) void k_merge_final(const uint32_t* __restrict__ part0,
+                                                     const uint32_t* __restrict__ part1,
+                                                     const uint32_t* __restrict__ off, uint32_t nb, uint32_t S2,
+                                                     int levels, uint32_t* __restrict__ buckets) {
+  msmk::merge_final<F>(blockIdx.x * TPB + threadIdx.x, part0, part1, off, nb, S2, levels, buckets);
 }
 template <class F>
 __global__ __launch_bounds__(TPB) void k_reduce_first(const uint32_t* __restrict__ buckets, uint32_t nwin,
@@ -278,28 +280,29 @@ void MsmEngine::run(const uint32_t* points, const uint32_t* scalars, size_t n, u
       h_total_[slot] = total;  // every compacted entry is one mixed addition
       HIPX(hipMemcpyAsync(&h_counts_[3 * slot + 2], &off_a_[nb], 4, hipMemcpyDeviceToHost, st));
     }
-    // segmented merge levels: part_a/off_a -> part_b/off_b -> ...
-    uint32_t *pin = part_a_, *pout = part_b_, *oin = off_a_, *oout = off_b_;
+    // merge levels for heavy buckets only (part_a <-> part_b at each bucket's own base off_a[b])
     size_t bound = max_tasks_now;
     for (int lv = 0; lv < merge_levels_; ++lv) {
-      hipLaunchKernelGGL(k_seg_counts, dim3(grid_for(nbuckets_ + 1)), dim3(TPB), 0, st, oin, nb,
-                         (uint32_t)prm_.S2, cnt_);
+      hipLaunchKernelGGL(k_heavy_counts, dim3(grid_for(nbuckets_ + 1)), dim3(TPB), 0, st, off_a_, nb,
+                         (uint32_t)prm_.S2, lv, cnt_);
       stmp = scan_tmp_bytes_;
-      HIPX(hipcub::DeviceScan::ExclusiveSum(scan_tmp_, stmp, cnt_, oout, (int)(nbuckets_ + 1), st));
-      bound = (bound + prm_.S2 - 1) / prm_.S2 + nbuckets_;
+      HIPX(hipcub::DeviceScan::ExclusiveSum(scan_tmp_, stmp, cnt_, off_b_, (int)(nbuckets_ + 1), st));
+      bound = 2 * bound / prm_.S2 + 1;  // heavy c > S2  =>  ceil(c/S2) <= 2c/S2
+      const uint32_t* src = (lv & 1) ? part_b_ : part_a_;
+      uint32_t* dst = (lv & 1) ? part_a_ : part_b_;
       if (curve_ == Curve::G1)
-        hipLaunchKernelGGL(k_merge<Fq>, dim3(grid_for(bound)), dim3(TPB), 0, st, pin, oin, oout, nb,
-                           (uint32_t)prm_.S2, pout);
+        hipLaunchKernelGGL(k_merge_heavy<Fq>, dim3(grid_for(bound)), dim3(TPB), 0, st, src, off_a_, off_b_, nb,
+                           (uint32_t)prm_.S2, lv, dst);
       else
-        hipLaunchKernelGGL(k_merge<Fq2>, dim3(grid_for(bound)), dim3(TPB), 0, st, pin, oin, oout, nb,
-                           (uint32_t)prm_.S2, pout);
-      std::swap(pin, pout);
-      std::swap(oin, oout);
+        hipLaunchKernelGGL(k_merge_heavy<Fq2>, dim3(grid_for(bound)), dim3(TPB), 0, st, src, off_a_, off_b_, nb,
+                           (uint32_t)prm_.S2, lv, dst);
     }
     if (curve_ == Curve::G1)
-      hipLaunchKernelGGL(k_merge_final<Fq>, dim3(grid_for(nbuckets_)), dim3(TPB), 0, st, pin, oin, nb, buckets_);
+      hipLaunchKernelGGL(k_merge_final<Fq>, dim3(grid_for(nbuckets_)), dim3(TPB), 0, st, part_a_, part_b_, off_a_,
+                         nb, (uint32_t)prm_.S2, merge_levels_, buckets_);
     else
-      hipLaunchKernelGGL(k_merge_final<Fq2>, dim3(grid_for(nbuckets_)), dim3(TPB), 0, st, pin, oin, nb, buckets_);
+      hipLaunchKernelGGL(k_merge_final<Fq2>, dim3(grid_for(nbuckets_)), dim3(TPB), 0, st, part_a_, part_b_, off_a_,
+                         nb, (uint32_t)prm_.S2, merge_levels_, buckets_);
     }
   }
   // bucket reduction tree per window

@@ -13,8 +13,9 @@
 //                 straddle a bucket, so every thread does the same bounded work
 //                 whatever the scalar distribution (0/1-heavy witnesses put
 //                 most points into a single bucket).  Mixed XYZZ additions.
-//  5. merge     : fixed number of segmented-reduce levels fold the per-task
-//                 partials of each bucket to one value.
+//  5. merge     : buckets with more than S2 task partials ("heavy": the 0/1-rich
+//                 witness buckets) are folded by segmented merge levels that skip
+//                 every light bucket; then one thread per bucket sums what is left.
 //  6. reduce    : per window, sum_k (k+1) B_k by an L-ary tree of running sums.
 //  7. windows   : W window sums go to the host, which folds them by Horner.
 #pragma once

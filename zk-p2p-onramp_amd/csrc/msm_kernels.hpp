@@ -6,6 +6,8 @@
 namespace zkp {
 namespace msmk {
 
+ZDEV uint32_t umin(uint32_t a, uint32_t b) { return a < b ? a : b; }
+
 ZDEV bool scalar_geq_r(const uint32_t (&s)[9]) {
 #pragma unroll
   for (int i = 7; i >= 0; --i) {
@@ -94,13 +96,6 @@ ZDEV void task_counts(uint32_t b, const uint32_t* __restrict__ start, const uint
   cnt[b] = b == nb ? 0u : (end[b] - start[b] + S - 1) / S;
 }
 
-// cnt[b] = ceil((off[b+1]-off[b]) / S2) for b < nb, cnt[nb] = 0
-ZDEV void seg_counts(uint32_t b, const uint32_t* __restrict__ off, uint32_t nb, uint32_t S2,
-                    uint32_t* __restrict__ cnt) {
-  if (b > nb) return;
-  cnt[b] = b == nb ? 0u : (off[b + 1] - off[b] + S2 - 1) / S2;
-}
-
 // largest b in [0, nb) with off[b] <= t   (off[0] = 0 <= t < off[nb])
 ZDEV uint32_t seg_search(const uint32_t* __restrict__ off, uint32_t nb, uint32_t t) {
   uint32_t lo = 0, hi = nb;
@@ -121,7 +116,7 @@ ZDEV void accumulate(uint32_t t, const uint32_t* __restrict__ points, const uint
   if (t >= off[nb]) return;
   const uint32_t b = seg_search(off, nb, t);
   const uint32_t s0 = start[b] + (t - off[b]) * S;
-  const uint32_t s1 = min(end[b], s0 + S);
+  const uint32_t s1 = umin(end[b], s0 + S);
   Xyzz<F> acc = xyzz_inf<F>();
   for (uint32_t j = s0; j < s1; ++j) {
     const uint32_t v = vals[j];
@@ -132,26 +127,65 @@ ZDEV void accumulate(uint32_t t, const uint32_t* __restrict__ points, const uint
   store_xyzz(out, t, acc);
 }
 
-template <class F>
-ZDEV void merge(uint32_t t, const uint32_t* __restrict__ in, const uint32_t* __restrict__ in_off,
-                const uint32_t* __restrict__ out_off, uint32_t nb, uint32_t S2, uint32_t* __restrict__ out) {
-  if (t >= out_off[nb]) return;
-  const uint32_t b = seg_search(out_off, nb, t);
-  const uint32_t s0 = in_off[b] + (t - out_off[b]) * S2;
-  const uint32_t s1 = min(in_off[b + 1], s0 + S2);
-  Xyzz<F> acc = load_xyzz<F>(in, s0);
-  for (uint32_t j = s0 + 1; j < s1; ++j) xyzz_add(acc, load_xyzz<F>(in, j));
-  store_xyzz(out, t, acc);
+// ---- bucket merge: only "heavy" buckets (more than S2 partials) take merge levels.
+// The partials of bucket b live at [off[b], off[b] + c) of a ping-pong pair of buffers:
+// after k merge levels applied to it, in buffer k&1 (0 = accumulate output) with
+// c = count after k levels.  A level turns c > S2 partials into ceil(c / S2), written
+// at the same base off[b] of the other buffer; light buckets are never touched.
+
+// partial count of a bucket with c0 task partials after `levels` merge levels, and the
+// number of levels that actually applied to it
+ZDEV uint32_t merged_count(uint32_t c0, uint32_t S2, int levels, int& applied) {
+  uint32_t c = c0;
+  applied = 0;
+  for (int l = 0; l < levels && c > S2; ++l) {
+    c = (c + S2 - 1) / S2;
+    ++applied;
+  }
+  return c;
 }
 
-// one thread per bucket: fold all its partials into buckets[b] (infinity if none)
+// merge tasks of level `lvl` (0-based): cnt[b] = ceil(c/S2) if bucket b is still heavy, else 0
+ZDEV void heavy_counts(uint32_t b, const uint32_t* __restrict__ off, uint32_t nb, uint32_t S2, int lvl,
+                       uint32_t* __restrict__ cnt) {
+  if (b > nb) return;
+  if (b == nb) {
+    cnt[b] = 0;
+    return;
+  }
+  int applied;
+  const uint32_t c = merged_count(off[b + 1] - off[b], S2, lvl, applied);
+  cnt[b] = (applied == lvl && c > S2) ? (c + S2 - 1) / S2 : 0u;
+}
+
+// merge task t of level lvl: sums <= S2 consecutive partials of one heavy bucket
 template <class F>
-ZDEV void merge_final(uint32_t b, const uint32_t* __restrict__ in, const uint32_t* __restrict__ in_off, uint32_t nb,
+ZDEV void merge_heavy(uint32_t t, const uint32_t* __restrict__ src, const uint32_t* __restrict__ off,
+                      const uint32_t* __restrict__ hoff, uint32_t nb, uint32_t S2, int lvl,
+                      uint32_t* __restrict__ dst) {
+  if (t >= hoff[nb]) return;
+  const uint32_t b = seg_search(hoff, nb, t);
+  const uint32_t j = t - hoff[b];
+  int applied;
+  const uint32_t c = merged_count(off[b + 1] - off[b], S2, lvl, applied);
+  const uint32_t s0 = off[b] + j * S2;
+  const uint32_t s1 = off[b] + umin(c, (j + 1) * S2);
+  Xyzz<F> acc = load_xyzz<F>(src, s0);
+  for (uint32_t k = s0 + 1; k < s1; ++k) xyzz_add(acc, load_xyzz<F>(src, k));
+  store_xyzz(dst, off[b] + j, acc);
+}
+
+// one thread per bucket: fold its (<= S2) remaining partials into buckets[b] (infinity if none)
+template <class F>
+ZDEV void merge_final(uint32_t b, const uint32_t* __restrict__ part0, const uint32_t* __restrict__ part1,
+                      const uint32_t* __restrict__ off, uint32_t nb, uint32_t S2, int levels,
                       uint32_t* __restrict__ buckets) {
   if (b >= nb) return;
-  const uint32_t s0 = in_off[b], s1 = in_off[b + 1];
+  int applied;
+  const uint32_t c = merged_count(off[b + 1] - off[b], S2, levels, applied);
+  const uint32_t* in = (applied & 1) ? part1 : part0;
   Xyzz<F> acc = xyzz_inf<F>();
-  for (uint32_t j = s0; j < s1; ++j) xyzz_add(acc, load_xyzz<F>(in, j));
+  for (uint32_t j = off[b]; j < off[b] + c; ++j) xyzz_add(acc, load_xyzz<F>(in, j));
   store_xyzz(buckets, b, acc);
 }
 

@@ -5,6 +5,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <exception>
 #include <thread>
@@ -404,10 +405,10 @@ class DevicePipeline {
     // MsmEngine::run blocks its host thread once (the sort needs the nonzero-digit count),
     // so each stream is fed from its own host thread; otherwise the host would serialise
     // the streams at those syncs.
+    // ZKP_SERIAL=1 (profiling only) chains the three streams so every kernel runs alone.
     HIPX(hipStreamWaitEvent(s1_, ev_[1], 0));
-    HIPX(hipStreamWaitEvent(s2_, ev_[1], 0));
-    std::exception_ptr err[2];
-    std::thread t_g2([&] {
+    std::exception_ptr err[3];
+    auto g2_job = [&] {
       try {
         HIPX(hipSetDevice(dev_));
         HIPX(hipEventRecord(ev_[7], s1_));
@@ -416,10 +417,11 @@ class DevicePipeline {
       } catch (...) {
         err[0] = std::current_exception();
       }
-    });
-    std::thread t_g1([&] {
+    };
+    auto g1_job = [&] {
       try {
         HIPX(hipSetDevice(dev_));
+        HIPX(hipStreamWaitEvent(s2_, serial_ ? ev_[6] : ev_[1], 0));
         HIPX(hipEventRecord(ev_[9], s2_));
         g1a_->run(pa_, d_wit, h.n_vars, wa);
         g1a_->run(pb1_, d_wit, h.n_vars, wa + wina_);
@@ -428,18 +430,27 @@ class DevicePipeline {
       } catch (...) {
         err[1] = std::current_exception();
       }
-    });
+    };
     // s0: quotient (buildABC, 3 coset NTTs, joinABC) then the H MSM
-    std::exception_ptr err0;
-    try {
-      enqueue_quotient(d_wit);
-      g1h_->run(ph_, pscal_, h.domain_size, wh);
-    } catch (...) {
-      err0 = std::current_exception();
+    auto h_job = [&] {
+      try {
+        if (serial_) HIPX(hipStreamWaitEvent(s0_, ev_[8], 0));
+        enqueue_quotient(d_wit);
+        g1h_->run(ph_, pscal_, h.domain_size, wh);
+      } catch (...) {
+        err[2] = std::current_exception();
+      }
+    };
+    if (serial_) {
+      g2_job();
+      if (!err[0]) g1_job();
+      if (!err[0] && !err[1]) h_job();
+    } else {
+      std::thread t_g2(g2_job), t_g1(g1_job);
+      h_job();
+      t_g2.join();
+      t_g1.join();
     }
-    t_g2.join();
-    t_g1.join();
-    if (err0) std::rethrow_exception(err0);
     for (auto& e : err)
       if (e) std::rethrow_exception(e);
     HIPX(hipEventRecord(ev_[4], s0_));
@@ -471,6 +482,7 @@ class DevicePipeline {
 
  private:
   int dev_;
+  bool serial_ = std::getenv("ZKP_SERIAL") && std::getenv("ZKP_SERIAL")[0] == '1';  // profiling: no stream overlap
   ZkeyHeader hdr_;
   hipStream_t s0_ = nullptr, s1_ = nullptr, s2_ = nullptr;
   hipEvent_t ev_[12];
