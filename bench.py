@@ -160,6 +160,7 @@ def main():
         elapsed = float(t.item())
         dist.barrier()
     kstats = prover.kernel_stats()
+    msm_cfg = prover.msm_config()
     stage_ms = prover.timings()
 
     # H2D-inclusive latency of one proof from a host witness (reported beside, never `value`)
@@ -212,7 +213,7 @@ def main():
         "config": {"workload": "configs[2]: full Groth16 prove, Venmo-shaped circuit, 1 proof per step",
                    "n_vars": circ.n_vars, "n_constraints": circ.n_constraints, "n_public": circ.n_public,
                    "domain": circ.domain_size, "distinct_witnesses_per_rank": nw,
-                   "parallelism": "replicas%d" % world},
+                   "parallelism": "replicas%d" % world, "msm": msm_cfg},
         "stage_ms_last_proof": {k: round(v, 3) for k, v in stage_ms.items()},
         "roofline": roofline,
     }

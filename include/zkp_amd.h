@@ -108,6 +108,11 @@ zkp_status zkp_msm_g1(int device, const uint8_t* points, const uint8_t* scalars,
                       int* is_inf);
 zkp_status zkp_msm_g2(int device, const uint8_t* points, const uint8_t* scalars, size_t n, uint8_t* out128,
                       int* is_inf);
+/* The same MSM with explicit Pippenger parameters (tests / tuning): window_bits c
+ * (0 = automatic, else 2..24) and base-table depth T (0 = automatic = all windows in
+ * one bucket set; 1 = no precomputed rows, one bucket group per window). */
+zkp_status zkp_msm(int device, int g2, const uint8_t* points, const uint8_t* scalars, size_t n, int window_bits,
+                   int table_depth, uint8_t* out, int* is_inf);
 /* In-place Fr transforms on n = 2^k standard-form LE elements, natural order:
  * mode 0: forward (A_j = sum a_i w^ij), 1: inverse, 2: coset-extend (snarkjs
  * ifft -> batchApplyKey(1, Fr.w[k+1]) -> fft). */
@@ -126,6 +131,10 @@ zkp_status zkp_prove_staged(zkp_prover* p, int dev_index, int slot, const uint8_
  * additions, [3] G1 tasks, [4..7] the same for G2.  Enabling resets the counters. */
 zkp_status zkp_prover_instrument(zkp_prover* p, int on);
 zkp_status zkp_prover_kernel_stats(const zkp_prover* p, double* out, int n);
+/* MSM configuration chosen at load (device 0): [0] witness-MSM window bits c, [1] its
+ * base-table depth T, [2] its bucket groups ceil(W/T), [3..5] the same for the H MSM,
+ * [6] bytes of precomputed base tables per device. */
+zkp_status zkp_prover_msm_config(const zkp_prover* p, double* out, int n);
 /* Device-resident kernel benchmarks.  MSM: stats[0] ms per MSM, [1] ms per
  * accumulate-kernel launch, [2] mixed additions per launch, [3] tasks per launch,
  * [4] window bits c, [5] windows.  out/is_inf receive the result (verification). */

@@ -100,3 +100,33 @@ def test_quotient_golden(golden_dir, name):
     p = zkp_amd.Prover(zk)
     want = [bn254.le_to_int(q[32 * i:32 * i + 32]) for i in range(len(q) // 32)]
     assert p.quotient(wt) == want
+
+
+# Pippenger parameter variants: window bits c and base-table depth T (T = W: one shared
+# bucket set over precomputed 2^(c t) P rows; T = 1: one bucket group per window;
+# 1 < T < W: several groups folded by Horner with shift c*T).  Bit-exact vs the oracle.
+@pytest.mark.parametrize("c,depth", [(0, 1), (5, 0), (5, 3), (8, 7), (13, 0), (2, 0), (20, 0)])
+def test_msm_g1_params(c, depth):
+    pts = _pts(200, 5)
+    rng = circuit.SplitMix64(6, 1)
+    sc = [rng.fr() for _ in range(200)]
+    pb, sb = _blob(pts, sc)
+    assert zkp_amd.msm_g1(pb, sb, window_bits=c, table_depth=depth) == groth16.msm_g1(pts, sc)
+
+
+def test_msm_g1_every_digit_one():
+    # every window digit of every scalar is 1 -> all n*W entries land in ONE bucket of the
+    # shared set: exercises the heavy-bucket merge levels
+    pts = _pts(200, 8)
+    s = sum(1 << (8 * w) for w in range(31))
+    pb, sb = _blob(pts, [s] * 200)
+    assert zkp_amd.msm_g1(pb, sb, window_bits=8) == groth16.msm_g1(pts, [s % R] * 200)
+
+
+@pytest.mark.parametrize("c,depth", [(0, 1), (6, 0), (6, 4)])
+def test_msm_g2_params(golden_dir, c, depth):
+    n = 64
+    pts, scal, exp = _load_msm(golden_dir, "msm_g2_%d.bin" % n, n, True)
+    v = [bn254.le_to_int(exp[32 * i:32 * i + 32]) for i in range(4)]
+    want = None if not any(exp) else ((v[0], v[1]), (v[2], v[3]))
+    assert zkp_amd.msm_g2(pts, scal, window_bits=c, table_depth=depth) == want

@@ -1,6 +1,6 @@
 // CPU replay of the MSM pipeline (msm_kernels.hpp per-thread bodies, same
 // parameters as MsmEngine) for debugging without a GPU.
-// usage: msm_emu <g1|g2> <file: points(zkey layout)|scalars> <n>   -> prints affine result (hex words)
+// usage: msm_emu <g1|g2> <file: points(zkey layout)|scalars> <n> [c] [depth]   -> prints affine result (hex words)
 #include <algorithm>
 #include <cstdio>
 #include <numeric>
@@ -11,7 +11,7 @@
 using namespace zkp;
 
 template <class F, class HF>
-static host::Jac<HF> run(std::vector<uint32_t>& pts, std::vector<uint32_t>& sc, uint32_t n) {
+static host::Jac<HF> run(std::vector<uint32_t>& pts, std::vector<uint32_t>& sc, uint32_t n, int c_ovr, int d_ovr) {
   constexpr int FW = FWords<F>::W;
   // convert points to device layout
   for (size_t i = 0; i < pts.size() / 8; ++i) {
@@ -19,19 +19,21 @@ static host::Jac<HF> run(std::vector<uint32_t>& pts, std::vector<uint32_t>& sc, 
     x = mul(x, fe_const<FqCfg>(Conv::FQ_ZKEY_TO_DEV));
     store_fe(&pts[i * 8], x);
   }
-  MsmParams prm = MsmParams::for_size(std::max<uint32_t>(n, 1));
-  const uint32_t W = prm.windows, half = 1u << (prm.c - 1), nb = W * half;
+  MsmParams prm = MsmParams::make(std::max<uint32_t>(n, 1), c_ovr, d_ovr);
+  const uint32_t W = prm.windows, T = prm.depth, G = prm.groups, half = 1u << (prm.c - 1), nb = G * half;
+  // base table rows 1..T-1 (as MsmBases::extend)
+  std::vector<uint32_t> table((size_t)T * n * 2 * FW);
+  std::copy(pts.begin(), pts.begin() + (size_t)n * 2 * FW, table.begin());
+  for (uint32_t t = 1; t < T; ++t)
+    for (uint32_t i = 0; i < n; ++i) msmk::extend_row<F>(i, table.data(), n, prm.c, (int)t);
   // compacted digit emission (window-major, point order) as k_digit_count/k_digit_write
   std::vector<std::vector<std::pair<uint32_t, uint32_t>>> per(W);
   for (uint32_t i = 0; i < n; ++i) {
     uint32_t s[9];
     msmk::load_scalar(sc.data(), i, s);
-    uint32_t carry = 0;
-    bool neg;
-    for (uint32_t w = 0; w < W; ++w) {
-      uint32_t key = msmk::digit_key(s, (int)w, prm.c, carry, neg, 0xffffffffu);
-      if (key != 0xffffffffu) per[w].push_back({key, i | (neg ? 0x80000000u : 0u)});
-    }
+    uint32_t carry = 0, key, val;
+    for (uint32_t w = 0; w < W; ++w)
+      if (msmk::digit_entry(s, (int)w, prm.c, (int)T, n, i, carry, key, val)) per[w].push_back({key, val});
   }
   std::vector<uint32_t> ks, vs;
   for (auto& v : per)
@@ -49,10 +51,9 @@ static host::Jac<HF> run(std::vector<uint32_t>& pts, std::vector<uint32_t>& sc, 
   for (uint32_t b = 0; b <= nb; ++b) { off[b] = acc; acc += cnt[b]; }
   const uint32_t ntask = off[nb];
   std::vector<uint32_t> part((size_t)(ntask + 1) * 4 * FW);
-  for (uint32_t t = 0; t < ntask; ++t) msmk::accumulate<F>(t, pts.data(), vs.data(), st.data(), en.data(), off.data(), nb, prm.S, part.data());
-  // heavy-bucket merge levels (as MsmEngine::run)
-  int levels = 0;
-  for (size_t m = (n + prm.S - 1) / prm.S; m > (size_t)prm.S2; m = (m + prm.S2 - 1) / prm.S2) ++levels;
+  for (uint32_t t = 0; t < ntask; ++t) msmk::accumulate<F>(t, table.data(), vs.data(), st.data(), en.data(), off.data(), nb, prm.S, part.data());
+  // heavy-bucket merge levels (as MsmPlan::build + MsmEngine::run)
+  const int levels = msm_merge_levels(std::max<uint32_t>(n, 1), prm);
   std::vector<uint32_t> part1(part.size()), hcnt(nb + 1), hoff(nb + 1);
   for (int lv = 0; lv < levels; ++lv) {
     for (uint32_t b = 0; b <= nb; ++b) msmk::heavy_counts(b, off.data(), nb, prm.S2, lv, hcnt.data());
@@ -65,19 +66,22 @@ static host::Jac<HF> run(std::vector<uint32_t>& pts, std::vector<uint32_t>& sc, 
   std::vector<uint32_t> buckets((size_t)nb * 4 * FW);
   for (uint32_t b = 0; b < nb; ++b)
     msmk::merge_final<F>(b, part.data(), part1.data(), off.data(), nb, prm.S2, levels, buckets.data());
-  uint32_t nodes = (half + prm.L - 1) / prm.L;
-  std::vector<uint32_t> s0((size_t)W * nodes * 4 * FW), t0(s0.size()), s1(s0.size()), t1(s0.size());
-  for (uint32_t id = 0; id < W * nodes; ++id) msmk::reduce_first<F>(id, buckets.data(), W, half, prm.L, s0.data(), t0.data());
-  int lgw = 3;
-  while (nodes > 1) {
-    uint32_t next = (nodes + prm.L - 1) / prm.L;
-    for (uint32_t id = 0; id < W * next; ++id) msmk::reduce_level<F>(id, s0.data(), t0.data(), W, nodes, prm.L, lgw, s1.data(), t1.data());
-    std::swap(s0, s1); std::swap(t0, t1);
-    nodes = next; lgw += 3;
+  // reduction (as run_engine): segments, subset sums, L-ary tree
+  const uint32_t M = prm.M, lgP = prm.lgP(), K = prm.K(), fan = prm.L, P = half / M;
+  std::vector<uint32_t> ss((size_t)G * P * 4 * FW), tt(ss.size());
+  for (uint32_t id = 0; id < G * P; ++id) msmk::reduce_segments<F>(id, buckets.data(), G, half, M, ss.data(), tt.data());
+  uint32_t nn = msmk::subset_n1(lgP, fan);
+  std::vector<uint32_t> sub((size_t)G * K * nn * 4 * FW), sub2(sub.size());
+  for (uint32_t id = 0; id < G * K * nn; ++id) msmk::subset_first<F>(id, ss.data(), tt.data(), G, lgP, fan, sub.data());
+  while (nn > 1) {
+    uint32_t next = (nn + fan - 1) / fan;
+    for (uint32_t id = 0; id < G * K * next; ++id) msmk::subset_level<F>(id, sub.data(), G * K, nn, fan, sub2.data());
+    std::swap(sub, sub2);
+    nn = next;
   }
-  // fold windows on host (same as prover.hip fold_windows)
+  // host fold (same as prover.hip msm_fold)
   auto ld = [&](uint32_t w) {
-    const uint32_t* p = t0.data() + (size_t)w * 4 * FW;
+    const uint32_t* p = sub.data() + (size_t)w * 4 * FW;
     if constexpr (FW == 8)
       return host::jac_from_xyzz(host::fq_from_dev(p), host::fq_from_dev(p + 8), host::fq_from_dev(p + 16), host::fq_from_dev(p + 24));
     else {
@@ -85,10 +89,16 @@ static host::Jac<HF> run(std::vector<uint32_t>& pts, std::vector<uint32_t>& sc, 
       return host::jac_from_xyzz(f2(p), f2(p + 16), f2(p + 32), f2(p + 48));
     }
   };
-  host::Jac<HF> r = ld(W - 1);
-  for (int w = (int)W - 2; w >= 0; --w) {
-    for (int i = 0; i < prm.c; ++i) r = host::jac_dbl(r);
-    r = host::jac_add(r, ld(w));
+  auto group = [&](uint32_t g) {
+    host::Jac<HF> a = lgP > 0 ? ld(g * K + lgP - 1) : host::Jac<HF>::inf();
+    for (int b = (int)lgP - 2; b >= 0; --b) a = host::jac_add(host::jac_dbl(a), ld(g * K + b));
+    for (int i = 0; i < prm.lg_m(); ++i) a = host::jac_dbl(a);
+    return host::jac_add(a, ld(g * K + lgP));
+  };
+  host::Jac<HF> r = group(G - 1);
+  for (int g = (int)G - 2; g >= 0; --g) {
+    for (int i = 0; i < prm.c * (int)T; ++i) r = host::jac_dbl(r);
+    r = host::jac_add(r, group(g));
   }
   return r;
 }
@@ -97,17 +107,18 @@ int main(int argc, char** argv) {
   bool g2 = std::string(argv[1]) == "g2";
   FILE* f = fopen(argv[2], "rb");
   uint32_t n = atoi(argv[3]);
+  const int c_ovr = argc > 4 ? atoi(argv[4]) : 0, d_ovr = argc > 5 ? atoi(argv[5]) : 0;
   size_t pw = g2 ? 32 : 16;
   std::vector<uint32_t> pts(n * pw), sc(n * 8 + 8);
   if (fread(pts.data(), 4, pts.size(), f) != pts.size()) return 1;
   if (fread(sc.data(), 4, n * 8, f) != n * 8) return 1;
   if (!g2) {
-    auto a = host::jac_to_aff(run<Fq, host::Fq>(pts, sc, n));
+    auto a = host::jac_to_aff(run<Fq, host::Fq>(pts, sc, n, c_ovr, d_ovr));
     if (a.inf) { printf("inf\n"); return 0; }
     auto x = a.x.to_std(), y = a.y.to_std();
     printf("%s %s\n", host::u256_to_dec(x).c_str(), host::u256_to_dec(y).c_str());
   } else {
-    auto a = host::jac_to_aff(run<Fq2, host::Fq2>(pts, sc, n));
+    auto a = host::jac_to_aff(run<Fq2, host::Fq2>(pts, sc, n, c_ovr, d_ovr));
     if (a.inf) { printf("inf\n"); return 0; }
     printf("%s %s %s %s\n", host::u256_to_dec(a.x.c0.to_std()).c_str(), host::u256_to_dec(a.x.c1.to_std()).c_str(),
            host::u256_to_dec(a.y.c0.to_std()).c_str(), host::u256_to_dec(a.y.c1.to_std()).c_str());

@@ -170,6 +170,21 @@ ZDEV Xyzz<F> xyzz_neg(const Xyzz<F>& p) {
   return r;
 }
 
+// XYZZ -> affine (x = X/ZZ, y = Y/ZZZ) with one inversion of ZZ*ZZZ; infinity -> (0, 0)
+template <class F>
+ZDEV Aff<F> xyzz_to_aff(const Xyzz<F>& p) {
+  Aff<F> a;
+  if (xyzz_is_inf(p)) {
+    a.x = f_zero<F>();
+    a.y = f_zero<F>();
+    return a;
+  }
+  const F I = inv(mul(p.zz, p.zzz));
+  a.x = mul(p.x, mul(p.zzz, I));
+  a.y = mul(p.y, mul(p.zz, I));
+  return a;
+}
+
 // ---------------------------------------------------------------- storage (HBM) layouts
 // G1 affine: 16 words (x, y), each 8 LE words.  G2 affine: 32 words (x.c0, x.c1, y.c0, y.c1).
 // XYZZ: 4 coordinates in the same order.

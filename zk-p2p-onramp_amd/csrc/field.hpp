@@ -262,6 +262,21 @@ ZDEV Fe<C> from_mont(const Fe<C>& a) {
   return canon(mul(a, one));
 }
 
+// a^(m-2) = a^-1 (Fermat), Montgomery form in and out; 0 -> 0.  Square-and-multiply
+// over the fixed exponent: ~254 S + ~130 M.  Load-time only (base-table precompute).
+template <class C>
+ZDEV Fe<C> inv(const Fe<C>& a) {
+  Fe<C> r = fe_one<C>();
+  for (int wi = 7; wi >= 0; --wi) {
+    const uint32_t e = C::MOD_W[wi] - (wi == 0 ? 2u : 0u);
+    for (int b = 31; b >= 0; --b) {
+      r = sqr(r);
+      if ((e >> b) & 1u) r = mul(r, a);
+    }
+  }
+  return r;
+}
+
 // ---------------------------------------------------------------- Fq2 = Fq[u]/(u^2+1)
 
 struct Fq2 {
@@ -293,5 +308,10 @@ ZDEV Fq2 sub(const Fq2& a, const Fq2& b) { return Fq2{sub(a.c0, b.c0), sub(a.c1,
 ZDEV Fq2 dbl(const Fq2& a) { return add(a, a); }
 ZDEV bool is_zero(const Fq2& a) { return is_zero(a.c0) && is_zero(a.c1); }
 ZDEV bool is_zero_raw(const Fq2& a) { return is_zero_raw(a.c0) && is_zero_raw(a.c1); }
+// (c0 + c1 u)^-1 = (c0 - c1 u) / (c0^2 + c1^2)
+ZDEV Fq2 inv(const Fq2& a) {
+  const Fq t = inv(add(sqr(a.c0), sqr(a.c1)));
+  return Fq2{mul(a.c0, t), mul(sub(fe_zero<FqCfg>(), a.c1), t)};
+}
 
 }  // namespace zkp

@@ -3,21 +3,37 @@
 // Replaces ffjavascript ``G1.multiExpAffine`` / ``G2.multiExpAffine``
 // (g1m/g2m_multiexpAffine_chunk) as called five times by
 // snarkjs ``groth16_prove``.  Result is bit-identical as a group element; the
-// algorithm is a GPU re-design, not a translation:
+// algorithm is a GPU re-design, not a translation.  Three objects:
 //
-//  1. digits    : one thread per scalar writes W signed c-bit digits as
-//                 (key = window*2^(c-1) + |d|-1, val = point | sign<<31).
-//  2. sort      : radix sort of the (key, val) pairs -> points grouped by bucket.
-//  3. bounds    : bucket [start, end) ranges from the sorted keys.
-//  4. accumulate: the sorted list is cut into tasks of <= S entries that never
-//                 straddle a bucket, so every thread does the same bounded work
-//                 whatever the scalar distribution (0/1-heavy witnesses put
-//                 most points into a single bucket).  Mixed XYZZ additions.
-//  5. merge     : buckets with more than S2 task partials ("heavy": the 0/1-rich
-//                 witness buckets) are folded by segmented merge levels that skip
-//                 every light bucket; then one thread per bucket sums what is left.
-//  6. reduce    : per window, sum_k (k+1) B_k by an L-ary tree of running sums.
-//  7. windows   : W window sums go to the host, which folds them by Horner.
+//  MsmBases  (per point set, built once at zkey load, resident in HBM)
+//     depth T rows of the affine bases: row t = 2^(c*t) * P_i.  With T = W
+//     (the default: 288 GB of HBM pays for it) every window of a scalar lands
+//     in ONE shared set of 2^(c-1) buckets, so the per-window bucket reduction
+//     and the host Horner fold disappear; with T < W the W windows fall into
+//     G = ceil(W/T) bucket groups, folded by Horner with shift c*T.
+//
+//  MsmPlan   (per scalar vector, per proof; shared by every MSM over the same
+//     scalars -- A, B1, C and the G2 MSM B2 all use the witness)
+//     1. digits : compacted emission of the nonzero signed c-bit digits as
+//                 (key = group*2^(c-1) + |d|-1, val = (t*n + i) | sign<<31),
+//                 window-major, point order within a window.
+//     2. sort   : stable radix sort on the c-1 bucket bits (groups stay grouped).
+//     3. bounds : bucket [start, end) ranges, accumulate-task offsets (tasks of
+//                 <= S entries never straddle a bucket) and the offsets of the
+//                 heavy-bucket merge levels.
+//
+//  MsmEngine (per curve and stream: partial sums, buckets, reduction tree)
+//     4. accumulate: one thread per task, mixed XYZZ additions of gathered bases;
+//                 every thread does the same bounded work whatever the scalar
+//                 distribution (0/1-heavy witnesses put most points in one bucket).
+//     5. merge  : buckets with more than S2 task partials are folded by segmented
+//                 merge levels that skip the light buckets; one thread per bucket
+//                 sums what is left.
+//     6. reduce : per group, sum_k (k+1) B_k = sum_p T_p + M sum_b 2^b Q_b from
+//                 segment running sums (S_p, T_p over M buckets) and bit-subset
+//                 sums Q_b = sum_{p: bit b} S_p, all plain L-ary tree sums.
+//     7. out    : G x K points (XYZZ, device layout); the host applies the 2^b, M
+//                 and group (2^(c T g)) weights by Horner (msm_fold).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cstddef>
@@ -28,42 +44,133 @@ namespace zkp {
 
 struct MsmParams {
   int c = 16;        // window bits
-  int windows = 16;  // ceil(255 / c)
-  int S = 32;        // max points per accumulate task
-  int S2 = 32;       // fan-in of a merge level
-  int L = 8;         // fan-in of a bucket-reduction level
-  static MsmParams for_size(size_t n) {
+  int windows = 16;  // W = ceil(255 / c)   (254-bit scalars + the signed-digit carry)
+  int depth = 16;    // T: precomputed rows per base
+  int groups = 1;    // G = ceil(W / T) bucket groups
+  int S = 32;        // max entries per accumulate task
+  int S2 = 4;        // fan-in of a heavy-bucket merge level (short chains: latency-bound)
+  int M = 4;         // buckets per reduction segment (running sums)
+  int L = 8;         // fan-in of a subset-sum tree level
+  // c_override / depth_override: 0 = automatic
+  static MsmParams make(size_t n, int c_override = 0, int depth_override = 0) {
     MsmParams p;
     int lg = 0;
     while ((size_t(1) << lg) < n) ++lg;
-    // bucket count 2^(c-1) per window ~ n/16..n/32 keeps buckets ~16-32 deep
-    p.c = lg - 3 < 8 ? 8 : (lg - 3 > 16 ? 16 : lg - 3);
+    // one bucket set of 2^(c-1) buckets against n*W entries: c = lg - 3 keeps every
+    // bucket ~16*W entries deep and the bucket reduction (2^c full adds) < 2% of the
+    // accumulation; 20 bits caps the sort at three 8-bit passes.
+    p.c = c_override > 0 ? c_override : (lg - 3 < 8 ? 8 : (lg - 3 > 20 ? 20 : lg - 3));
+    if (p.c < 2) p.c = 2;
+    if (p.c > 24) p.c = 24;
     p.windows = (255 + p.c - 1) / p.c;
+    p.depth = depth_override > 0 ? (depth_override < p.windows ? depth_override : p.windows) : p.windows;
+    p.groups = (p.windows + p.depth - 1) / p.depth;
+    if (p.M > (1 << (p.c - 1))) p.M = 1 << (p.c - 1);
     return p;
   }
+  // reduction output: per group, lgP subset sums Q_b and sum_p T_p (P = 2^(c-1) / M segments)
+  int lg_m() const { int l = 0; while ((1 << l) < M) ++l; return l; }
+  int lgP() const { return c - 1 - lg_m(); }
+  int K() const { return lgP() + 1; }
+  size_t half() const { return size_t(1) << (c - 1); }
+  size_t buckets() const { return (size_t)groups * half(); }
 };
 
 // words per coordinate element: G1 -> Fq (8 words), G2 -> Fq2 (16 words)
 enum class Curve { G1 = 1, G2 = 2 };
 
+inline int curve_fwords(Curve c) { return c == Curve::G1 ? 8 : 16; }
+
+// Precomputed base table: rows() x n affine points (device layout, Montgomery R'=2^261).
+class MsmBases {
+ public:
+  MsmBases(Curve curve, size_t n, int c, int depth);
+  ~MsmBases();
+  MsmBases(const MsmBases&) = delete;
+  MsmBases& operator=(const MsmBases&) = delete;
+  // row 0 (n points): the caller fills it (device layout), then extend() derives rows 1..T-1
+  uint32_t* row0() { return d_; }
+  void extend(hipStream_t st);
+  const uint32_t* data() const { return d_; }
+  size_t n() const { return n_; }
+  int c() const { return c_; }
+  int depth() const { return depth_; }
+  Curve curve() const { return curve_; }
+  size_t bytes() const { return bytes_; }
+  static size_t bytes_for(Curve curve, size_t n, int depth) {
+    return (size_t)depth * (n ? n : 1) * 8 * curve_fwords(curve);
+  }
+
+ private:
+  Curve curve_;
+  size_t n_;
+  int c_, depth_;
+  size_t bytes_ = 0;
+  uint32_t* d_ = nullptr;
+};
+
+class MsmPlan {
+ public:
+  MsmPlan(size_t max_n, const MsmParams& prm, hipStream_t stream);
+  ~MsmPlan();
+  MsmPlan(const MsmPlan&) = delete;
+  MsmPlan& operator=(const MsmPlan&) = delete;
+  // scalars: device, 8 LE 32-bit words each (standard form, any value < 2^256).
+  // Enqueues on the plan's stream and blocks the host once (the sort needs the
+  // number of nonzero digits); records ready() at the end.
+  void build(const uint32_t* scalars, size_t n);
+  const MsmParams& params() const { return prm_; }
+  hipEvent_t ready() const { return ready_; }
+  hipStream_t stream() const { return stream_; }
+  size_t n() const { return n_; }
+  size_t max_n() const { return max_n_; }
+  uint32_t entries() const { return total_; }  // nonzero digits = mixed additions per MSM
+  int merge_levels() const { return merge_levels_; }
+
+  // device results (read-only once ready())
+  const uint32_t* vals() const { return vals_sorted_; }
+  const uint32_t* bstart() const { return bstart_; }
+  const uint32_t* bend() const { return bend_; }
+  const uint32_t* task_off() const { return off_task_; }
+  const uint32_t* level_off(int lv) const { return off_lvl_[lv]; }
+  size_t max_tasks_now() const { return max_tasks_now_; }
+  size_t max_tasks() const { return max_tasks_; }
+
+ private:
+  MsmParams prm_;
+  size_t max_n_, n_ = 0;
+  hipStream_t stream_;
+  hipEvent_t ready_ = nullptr;
+  size_t nbuckets_ = 0, max_entries_ = 0, max_tasks_ = 0, max_tasks_now_ = 0;
+  int merge_levels_ = 0;
+  uint32_t total_ = 0;
+  uint32_t *keys_ = nullptr, *vals_ = nullptr, *keys_sorted_ = nullptr, *vals_sorted_ = nullptr;
+  uint32_t *bstart_ = nullptr, *bend_ = nullptr, *cnt_ = nullptr, *off_task_ = nullptr;
+  std::vector<uint32_t*> off_lvl_;
+  uint32_t *bcnt_ = nullptr, *boff_ = nullptr;  // per (window, digit block) counts / offsets
+  uint32_t* h_valid_ = nullptr;                 // pinned: number of nonzero digits
+  void* sort_tmp_ = nullptr;
+  size_t sort_tmp_bytes_ = 0;
+  void* scan_tmp_ = nullptr;
+  size_t scan_tmp_bytes_ = 0;
+};
+
 class MsmEngine {
  public:
-  MsmEngine(Curve curve, size_t max_n, hipStream_t stream);
+  MsmEngine(Curve curve, const MsmParams& prm, size_t max_n, hipStream_t stream);
   ~MsmEngine();
   MsmEngine(const MsmEngine&) = delete;
   MsmEngine& operator=(const MsmEngine&) = delete;
 
-  // points: device, affine, device layout (Montgomery R'=2^261, 8 LE words per Fq).
-  // scalars: device, 8 LE 32-bit words per scalar (standard form, any value < 2^256).
-  // Enqueues the whole pipeline on the engine's stream; the W window sums (XYZZ,
-  // device layout, window_words() words) land in d_out (device).  Nothing is
-  // synchronised: the caller orders/awaits the stream.
-  void run(const uint32_t* points, const uint32_t* scalars, size_t n, uint32_t* d_out);
-  size_t window_words() const { return (size_t)prm_.windows * 4 * fwords_; }
+  // sum_i s_i * P_i for the plan's scalars over the bases (bases.n() == plan.n(),
+  // same c and depth).  Waits for plan.ready() on the engine's stream, enqueues
+  // everything there; the G group sums (XYZZ, device layout, window_words() words)
+  // land in d_out (device).  Nothing is synchronised.
+  void run(const MsmPlan& plan, const MsmBases& bases, uint32_t* d_out);
+  size_t window_words() const { return (size_t)prm_.groups * prm_.K() * 4 * fwords_; }
 
   // Kernel instrumentation (HIP events on this engine's stream).  When enabled,
-  // every run() brackets the bucket-accumulate kernel with events and copies the
-  // number of nonzero digits (= mixed additions) to pinned memory.  collect()
+  // every run() brackets the bucket-accumulate kernel with events; collect()
   // must be called after the stream is synchronised.
   struct Stats {
     double accumulate_ms = 0;  // summed over launches
@@ -76,37 +183,34 @@ class MsmEngine {
   const MsmParams& params() const { return prm_; }
   Curve curve() const { return curve_; }
   hipStream_t stream() const { return stream_; }
-  size_t max_n() const { return max_n_; }
 
  private:
   Curve curve_;
+  MsmParams prm_;
   size_t max_n_;
   hipStream_t stream_;
-  MsmParams prm_;
-  size_t nbuckets_ = 0;     // windows * 2^(c-1)
-  size_t max_entries_ = 0;  // max_n * windows
-  size_t max_tasks_ = 0;
-  int merge_levels_ = 0;
-  // device buffers
-  uint32_t *keys_ = nullptr, *vals_ = nullptr, *keys_sorted_ = nullptr, *vals_sorted_ = nullptr;
-  uint32_t *bstart_ = nullptr, *bend_ = nullptr, *cnt_ = nullptr, *off_a_ = nullptr, *off_b_ = nullptr;
+  size_t nbuckets_ = 0, max_tasks_ = 0;
+  int fwords_;
   uint32_t *part_a_ = nullptr, *part_b_ = nullptr, *buckets_ = nullptr;
-  uint32_t *bcnt_ = nullptr, *boff_ = nullptr;  // compacted digit emission: per (window, block) counts/offsets
-  uint32_t* h_valid_ = nullptr;                 // pinned: number of nonzero digits of the current run
-  uint32_t last_valid_ = 0;
-  uint32_t *lvl_s_[2] = {nullptr, nullptr}, *lvl_t_[2] = {nullptr, nullptr};
-  void* sort_tmp_ = nullptr;
-  size_t sort_tmp_bytes_ = 0;
-  void* scan_tmp_ = nullptr;
-  size_t scan_tmp_bytes_ = 0;
-  int fwords_;  // words per field element (8 or 16)
-  // instrumentation
+  uint32_t *seg_s_ = nullptr, *seg_t_ = nullptr, *sub_[2] = {nullptr, nullptr};
   static constexpr int MAX_PENDING = 16;
   bool instrument_ = false;
   int pending_ = 0;
   hipEvent_t ev_[MAX_PENDING][2];
-  uint32_t* h_counts_ = nullptr;  // pinned: [invalid-bucket start, end, tasks] per pending run
+  uint32_t* h_counts_ = nullptr;  // pinned: tasks per pending run
   uint32_t h_total_[MAX_PENDING] = {};
 };
+
+// merge levels needed for n points with the given params (worst case: one bucket of
+// a group receives a digit of every window of the group)
+inline int msm_merge_levels(size_t max_n, const MsmParams& prm) {
+  size_t m = ((max_n ? max_n : 1) * (size_t)prm.depth + prm.S - 1) / prm.S;
+  int levels = 0;
+  while (m > (size_t)prm.S2) {
+    m = (m + prm.S2 - 1) / prm.S2;
+    ++levels;
+  }
+  return levels;
+}
 
 }  // namespace zkp

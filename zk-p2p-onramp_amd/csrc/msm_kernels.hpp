@@ -26,35 +26,6 @@ ZDEV void scalar_sub_r(uint32_t (&s)[9]) {
   }
 }
 
-ZDEV void digits(uint32_t i, const uint32_t* __restrict__ scalars, uint32_t n, int c, int W,
-                uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
-  if (i >= n) return;
-  const uint4* q = reinterpret_cast<const uint4*>(scalars + (size_t)i * 8);
-  uint4 a = q[0], b = q[1];
-  uint32_t s[9] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, 0u};
-  while (scalar_geq_r(s)) scalar_sub_r(s);  // snarkjs scalars are < r; others reduce (k*P == (k mod r)*P)
-  const uint32_t half = 1u << (c - 1), full = 1u << c, invalid = (uint32_t)W * half;
-  uint32_t carry = 0;
-  for (int w = 0; w < W; ++w) {
-    const int bit = w * c, j = bit >> 5, sh = bit & 31;
-    const uint64_t v = (uint64_t)s[j] | ((uint64_t)s[j + 1] << 32);
-    uint32_t raw = (uint32_t)(v >> sh) & (full - 1);
-    raw += carry;
-    uint32_t key, val = i;
-    if (raw > half) {
-      carry = 1;
-      const uint32_t mag = full - raw;  // digit = raw - 2^c <= 0 (0 when raw == 2^c: pure carry)
-      key = mag == 0 ? invalid : (uint32_t)w * half + mag - 1;
-      val |= 0x80000000u;
-    } else {
-      carry = 0;
-      key = raw == 0 ? invalid : (uint32_t)w * half + raw - 1;
-    }
-    keys[(size_t)w * n + i] = key;
-    vals[(size_t)w * n + i] = val;
-  }
-}
-
 // load scalar i as 9 words (word 8 = 0), reduced below r
 ZDEV void load_scalar(const uint32_t* __restrict__ scalars, uint32_t i, uint32_t (&s)[9]) {
   const uint4* q = reinterpret_cast<const uint4*>(scalars + (size_t)i * 8);
@@ -64,21 +35,46 @@ ZDEV void load_scalar(const uint32_t* __restrict__ scalars, uint32_t i, uint32_t
 }
 
 // signed c-bit digit of window w (windows visited in order, carry threaded through):
-// returns the key window*2^(c-1) + |d|-1, or `invalid` for a zero digit; neg = (d < 0)
-ZDEV uint32_t digit_key(const uint32_t (&s)[9], int w, int c, uint32_t& carry, bool& neg, uint32_t invalid) {
+// returns |d| (0 for a zero digit); neg = (d < 0)
+ZDEV uint32_t digit_mag(const uint32_t (&s)[9], int w, int c, uint32_t& carry, bool& neg) {
   const uint32_t half = 1u << (c - 1), full = 1u << c;
   const int bit = w * c, j = bit >> 5, sh = bit & 31;
-  const uint64_t v = (uint64_t)s[j] | ((uint64_t)s[j + 1] << 32);
+  const uint64_t v = (uint64_t)s[j] | ((uint64_t)s[j + 1] << 32);  // sh + c <= 31 + 24 < 64
   const uint32_t raw = ((uint32_t)(v >> sh) & (full - 1)) + carry;
   if (raw > half) {
     carry = 1;
     neg = true;
-    const uint32_t mag = full - raw;  // 0 when raw == 2^c: pure carry
-    return mag == 0 ? invalid : (uint32_t)w * half + mag - 1;
+    return full - raw;  // 0 when raw == 2^c: pure carry
   }
   carry = 0;
   neg = false;
-  return raw == 0 ? invalid : (uint32_t)w * half + raw - 1;
+  return raw;
+}
+
+// entry of window w of scalar i: bucket key = group*2^(c-1) + |d|-1 with group = w / T,
+// base index (t*n + i) | sign with t = w % T (row t of the table holds 2^(c t) P_i)
+ZDEV bool digit_entry(const uint32_t (&s)[9], int w, int c, int T, uint32_t n, uint32_t i, uint32_t& carry,
+                      uint32_t& key, uint32_t& val) {
+  bool neg;
+  const uint32_t mag = digit_mag(s, w, c, carry, neg);
+  const uint32_t g = (uint32_t)w / (uint32_t)T, t = (uint32_t)w - g * (uint32_t)T;
+  key = (g << (c - 1)) + mag - 1;
+  val = (t * n + i) | (neg ? 0x80000000u : 0u);
+  return mag != 0;
+}
+
+// row t of base i from row t-1: 2^c * P (affine; infinity stays all-zero)
+template <class F>
+ZDEV void extend_row(uint32_t i, uint32_t* __restrict__ table, uint32_t n, int c, int t) {
+  if (i >= n) return;
+  const Aff<F> p = load_aff<F>(table, (size_t)(t - 1) * n + i);
+  Aff<F> a = p;
+  if (!aff_is_inf(p)) {
+    Xyzz<F> q = xyzz_dbl_aff(p);
+    for (int k = 1; k < c; ++k) q = xyzz_dbl(q);
+    a = xyzz_to_aff(q);
+  }
+  store_aff(table, (size_t)t * n + i, a);
 }
 
 ZDEV void bounds(uint32_t i, const uint32_t* __restrict__ keys, uint32_t total, uint32_t* __restrict__ start,
@@ -189,51 +185,67 @@ ZDEV void merge_final(uint32_t b, const uint32_t* __restrict__ part0, const uint
   store_xyzz(buckets, b, acc);
 }
 
-// level 1 of the bucket reduction: node g of window w covers buckets [gL, gL+L):
-//   S = sum B_k,  T = sum (j+1) B_(gL+j)
+// ---- bucket reduction:  sum_k (k+1) B_k over the 2^(c-1) buckets of a group, as
+//   sum_p T_p + M * sum_b 2^b Q_b   with  S_p = sum_j B_(pM+j),  T_p = sum_j (j+1) B_(pM+j)
+//   (segments of M buckets) and Q_b = sum of S_p over the p with bit b set.
+// Every piece is a plain sum (no doublings inside the tree), so the latency is a few
+// short add chains instead of one long running sum; the host applies the 2^b / M weights.
+
+// segment p of group g (one thread): S_p, T_p by running sums over M buckets
 template <class F>
-ZDEV void reduce_first(uint32_t id, const uint32_t* __restrict__ buckets, uint32_t nwin, uint32_t half, uint32_t L,
-                       uint32_t* __restrict__ s_out, uint32_t* __restrict__ t_out) {
-  const uint32_t nodes = (half + L - 1) / L;
-  if (id >= nwin * nodes) return;
-  const uint32_t w = id / nodes, g = id - w * nodes;
+ZDEV void reduce_segments(uint32_t id, const uint32_t* __restrict__ buckets, uint32_t G, uint32_t half, uint32_t M,
+                          uint32_t* __restrict__ s_out, uint32_t* __restrict__ t_out) {
+  const uint32_t P = half / M;
+  if (id >= G * P) return;
+  const uint32_t g = id / P, p = id - g * P;
   Xyzz<F> R = xyzz_inf<F>(), T = xyzz_inf<F>();
-  for (int j = (int)L - 1; j >= 0; --j) {
-    const uint32_t k = g * L + (uint32_t)j;
-    if (k < half) xyzz_add(R, load_xyzz<F>(buckets, (size_t)w * half + k));
+  for (int j = (int)M - 1; j >= 0; --j) {
+    xyzz_add(R, load_xyzz<F>(buckets, (size_t)g * half + (size_t)p * M + (uint32_t)j));
     xyzz_add(T, R);
   }
   store_xyzz(s_out, id, R);
   store_xyzz(t_out, id, T);
 }
 
-// level l>1: node h of window w has children [hL, hL+L) of width 2^lg_width buckets:
-//   S' = sum S_j,  T' = sum T_j + 2^lg_width * sum j S_j
+// elements per first-level output of the subset sums (n1 outputs per sum)
+ZDEV uint32_t subset_n1(uint32_t lgP, uint32_t fan) {
+  const uint32_t P = 1u << lgP;
+  return (P + 2 * fan - 1) / (2 * fan);
+}
+
+// first level of the K = lgP + 1 subset sums of group g: sum b < lgP over the P/2 values
+// S_p with bit b of p set (fan consecutive per thread), sum lgP over all P values T_p
+// (2*fan per thread).  out[(g*K + b)*n1 + j]
 template <class F>
-ZDEV void reduce_level(uint32_t id, const uint32_t* __restrict__ s_in, const uint32_t* __restrict__ t_in,
-                       uint32_t nwin, uint32_t n_in, uint32_t L, int lg_width, uint32_t* __restrict__ s_out,
-                       uint32_t* __restrict__ t_out) {
-  const uint32_t nodes = (n_in + L - 1) / L;
-  if (id >= nwin * nodes) return;
-  const uint32_t w = id / nodes, h = id - w * nodes;
-  Xyzz<F> R = xyzz_inf<F>(), U = xyzz_inf<F>(), Tsum = xyzz_inf<F>();
-  for (int j = (int)L - 1; j >= 1; --j) {
-    const uint32_t k = h * L + (uint32_t)j;
-    if (k < n_in) {
-      xyzz_add(R, load_xyzz<F>(s_in, (size_t)w * n_in + k));
-      xyzz_add(Tsum, load_xyzz<F>(t_in, (size_t)w * n_in + k));
+ZDEV void subset_first(uint32_t id, const uint32_t* __restrict__ s_in, const uint32_t* __restrict__ t_in,
+                       uint32_t G, uint32_t lgP, uint32_t fan, uint32_t* __restrict__ out) {
+  const uint32_t P = 1u << lgP, K = lgP + 1, n1 = subset_n1(lgP, fan);
+  if (id >= G * K * n1) return;
+  const uint32_t seg = id / n1, j = id - seg * n1, g = seg / K, b = seg - g * K;
+  Xyzz<F> acc = xyzz_inf<F>();
+  if (b < lgP) {
+    const uint32_t lo = (1u << b) - 1;
+    for (uint32_t i = j * fan; i < umin((j + 1) * fan, P / 2); ++i) {
+      const uint32_t p = ((i >> b) << (b + 1)) | (1u << b) | (i & lo);
+      xyzz_add(acc, load_xyzz<F>(s_in, (size_t)g * P + p));
     }
-    xyzz_add(U, R);
+  } else {
+    for (uint32_t i = j * 2 * fan; i < umin((j + 1) * 2 * fan, P); ++i)
+      xyzz_add(acc, load_xyzz<F>(t_in, (size_t)g * P + i));
   }
-  {
-    const uint32_t k = h * L;
-    xyzz_add(R, load_xyzz<F>(s_in, (size_t)w * n_in + k));
-    xyzz_add(Tsum, load_xyzz<F>(t_in, (size_t)w * n_in + k));
-  }
-  for (int i = 0; i < lg_width; ++i) U = xyzz_dbl(U);
-  xyzz_add(Tsum, U);
-  store_xyzz(s_out, id, R);
-  store_xyzz(t_out, id, Tsum);
+  store_xyzz(out, id, acc);
+}
+
+// next level: nseg segments of n_in values -> n_out = ceil(n_in / fan) sums of fan consecutive
+template <class F>
+ZDEV void subset_level(uint32_t id, const uint32_t* __restrict__ in, uint32_t nseg, uint32_t n_in, uint32_t fan,
+                       uint32_t* __restrict__ out) {
+  const uint32_t n_out = (n_in + fan - 1) / fan;
+  if (id >= nseg * n_out) return;
+  const uint32_t seg = id / n_out, j = id - seg * n_out;
+  Xyzz<F> acc = xyzz_inf<F>();
+  for (uint32_t i = j * fan; i < umin((j + 1) * fan, n_in); ++i) xyzz_add(acc, load_xyzz<F>(in, (size_t)seg * n_in + i));
+  store_xyzz(out, id, acc);
 }
 
 }  // namespace msmk

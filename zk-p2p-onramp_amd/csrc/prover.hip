@@ -8,6 +8,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <exception>
+#include <future>
 #include <thread>
 
 #include "hip_check.hpp"
@@ -198,21 +199,30 @@ HFq2 f_from_dev<HFq2>(const uint32_t* w) {
   return fq2_from_dev(w);
 }
 
-// fold W window sums (XYZZ device layout) by Horner: sum_w 2^(c w) T_w
+// fold an MSM engine output (device XYZZ layout, G x K points: per group the lgP subset
+// sums Q_b then sum_p T_p) into the MSM value:
+//   R_g = sum_p T_p + M * sum_b 2^b Q_b,   result = sum_g 2^(c T g) R_g   (Horner both)
 template <class F>
-static Jac<F> fold_windows(const uint32_t* win, int W, int c) {
+static Jac<F> msm_fold(const uint32_t* win, const MsmParams& p) {
   constexpr int FW = sizeof(F) == sizeof(HFq) ? 8 : 16;
-  auto load = [&](int w) {
-    const uint32_t* p = win + (size_t)w * 4 * FW;
-    return host::jac_from_xyzz(f_from_dev<F>(p), f_from_dev<F>(p + FW), f_from_dev<F>(p + 2 * FW),
-                               f_from_dev<F>(p + 3 * FW));
+  auto load = [&](size_t k) {
+    const uint32_t* q = win + k * 4 * FW;
+    return host::jac_from_xyzz(f_from_dev<F>(q), f_from_dev<F>(q + FW), f_from_dev<F>(q + 2 * FW),
+                               f_from_dev<F>(q + 3 * FW));
   };
-  Jac<F> acc = load(W - 1);
-  for (int w = W - 2; w >= 0; --w) {
-    for (int i = 0; i < c; ++i) acc = host::jac_dbl(acc);
-    acc = host::jac_add(acc, load(w));
+  const int K = p.K(), lgP = p.lgP();
+  auto group = [&](int g) {
+    Jac<F> acc = lgP > 0 ? load((size_t)g * K + lgP - 1) : Jac<F>::inf();
+    for (int b = lgP - 2; b >= 0; --b) acc = host::jac_add(host::jac_dbl(acc), load((size_t)g * K + b));
+    for (int i = 0; i < p.lg_m(); ++i) acc = host::jac_dbl(acc);
+    return host::jac_add(acc, load((size_t)g * K + lgP));
+  };
+  Jac<F> r = group(p.groups - 1);
+  for (int g = p.groups - 2; g >= 0; --g) {
+    for (int i = 0; i < p.c * p.depth; ++i) r = host::jac_dbl(r);
+    r = host::jac_add(r, group(g));
   }
-  return acc;
+  return r;
 }
 
 static U256 scalar_or_random(const uint8_t* s32) {
@@ -240,32 +250,70 @@ static void put_fq(const HFq& x, uint8_t* out) { host::u256_to_le(x.to_std(), ou
 
 // ------------------------------------------------------------------ device pipeline
 
+static int env_int(const char* name, int dflt) {
+  const char* v = std::getenv(name);
+  return (v && *v) ? std::atoi(v) : dflt;
+}
+
+// MSM parameters for a prover: window bits automatic (ZKP_WINDOW_BITS overrides);
+// table depth = W (one bucket set) unless the tables would not fit in half of the free
+// HBM, then the largest depth that does (ZKP_TABLE_DEPTH overrides).
+static void choose_msm_params(size_t n_w, size_t n_h, MsmParams& pw, MsmParams& ph) {
+  const int c = env_int("ZKP_WINDOW_BITS", 0), d = env_int("ZKP_TABLE_DEPTH", 0);
+  pw = MsmParams::make(n_w, c, d);
+  ph = MsmParams::make(n_h, c, d);
+  if (d > 0) return;
+  size_t free_b = 0, total_b = 0;
+  HIPX(hipMemGetInfo(&free_b, &total_b));
+  const size_t row_w = n_w * (3 * 64 + 128), row_h = n_h * 64;
+  const size_t budget = free_b / 2;
+  int depth = std::max(pw.windows, ph.windows);
+  while (depth > 1 && (size_t)std::min(depth, pw.windows) * row_w + (size_t)std::min(depth, ph.windows) * row_h > budget)
+    --depth;
+  pw = MsmParams::make(n_w, c, depth);
+  ph = MsmParams::make(n_h, c, depth);
+}
+
+// upload `count` zkey points (snarkjs LEM layout) into row 0 of a base table at point
+// offset `at`, convert to the device Montgomery form, then derive the shifted rows
+static void fill_bases(MsmBases& b, const uint8_t* src, size_t count, size_t at, hipStream_t st) {
+  const size_t pw = b.curve() == Curve::G1 ? 16 : 32;  // words per point
+  if (at) HIPX(hipMemsetAsync(b.row0(), 0, at * pw * 4, st));  // leading infinity points
+  if (count) {
+    HIPX(hipMemcpyAsync(b.row0() + at * pw, src, count * pw * 4, hipMemcpyHostToDevice, st));
+    launch_convert_fq_zkey(b.row0() + at * pw, count * pw / 8, st);
+  }
+  b.extend(st);
+}
+
 class DevicePipeline {
  public:
   DevicePipeline(int dev, const ZkeyParsed& z) : dev_(dev), hdr_(z.hdr) {
     HIPX(hipSetDevice(dev_));
-    HIPX(hipStreamCreateWithFlags(&s0_, hipStreamNonBlocking));
-    HIPX(hipStreamCreateWithFlags(&s1_, hipStreamNonBlocking));
-    HIPX(hipStreamCreateWithFlags(&s2_, hipStreamNonBlocking));
+    // s0 carries the critical path (quotient -> H plan -> H MSM): highest priority, so the
+    // A/B1/C (s2) and B2 (s1) MSMs fill the CUs it leaves idle instead of delaying it
+    int prio_lo = 0, prio_hi = 0;
+    HIPX(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
+    HIPX(hipStreamCreateWithPriority(&s0_, hipStreamNonBlocking, prio_hi));
+    HIPX(hipStreamCreateWithPriority(&s1_, hipStreamNonBlocking, prio_lo));
+    HIPX(hipStreamCreateWithPriority(&s2_, hipStreamNonBlocking, prio_lo));
     for (auto& e : ev_) HIPX(hipEventCreate(&e));
     const ZkeyHeader& h = hdr_;
     const size_t nv = h.n_vars, nd = h.domain_size, nc = h.n_vars - h.n_public - 1;
-    auto up = [&](const Section& s, size_t bytes) {
-      uint32_t* d = nullptr;
-      HIPX(hipMalloc(&d, std::max<size_t>(bytes, 64)));
-      if (bytes) HIPX(hipMemcpyAsync(d, s.ptr, bytes, hipMemcpyHostToDevice, s0_));
-      return d;
-    };
-    pa_ = up(z.bf.sec[5], nv * 64);
-    pb1_ = up(z.bf.sec[6], nv * 64);
-    pb2_ = up(z.bf.sec[7], nv * 128);
-    pc_ = up(z.bf.sec[8], nc * 64);
-    ph_ = up(z.bf.sec[9], nd * 64);
-    launch_convert_fq_zkey(pa_, nv * 2, s0_);
-    launch_convert_fq_zkey(pb1_, nv * 2, s0_);
-    launch_convert_fq_zkey(pb2_, nv * 4, s0_);
-    launch_convert_fq_zkey(pc_, nc * 2, s0_);
-    launch_convert_fq_zkey(ph_, nd * 2, s0_);
+    MsmParams pw, ph;
+    choose_msm_params(nv, nd, pw, ph);
+    // base tables: A, B1, C, B2 indexed by witness signal (C's first nPublic+1 bases are
+    // infinity, so one witness plan serves all four), H by domain index
+    ta_ = std::make_unique<MsmBases>(Curve::G1, nv, pw.c, pw.depth);
+    tb1_ = std::make_unique<MsmBases>(Curve::G1, nv, pw.c, pw.depth);
+    tc_ = std::make_unique<MsmBases>(Curve::G1, nv, pw.c, pw.depth);
+    tb2_ = std::make_unique<MsmBases>(Curve::G2, nv, pw.c, pw.depth);
+    th_ = std::make_unique<MsmBases>(Curve::G1, nd, ph.c, ph.depth);
+    fill_bases(*ta_, z.bf.sec[5].ptr, nv, 0, s0_);
+    fill_bases(*tb1_, z.bf.sec[6].ptr, nv, 0, s0_);
+    fill_bases(*tb2_, z.bf.sec[7].ptr, nv, 0, s0_);
+    fill_bases(*tc_, z.bf.sec[8].ptr, nc, nv - nc, s0_);
+    fill_bases(*th_, z.bf.sec[9].ptr, nd, 0, s0_);
     for (int m = 0; m < 2; ++m) {
       const Csr& c = z.csr[m];
       HIPX(hipMalloc(&rowptr_[m], c.rowptr.size() * 4));
@@ -282,11 +330,13 @@ class DevicePipeline {
     for (auto& b : abc_) HIPX(hipMalloc(&b, nd * 32));
     HIPX(hipMalloc(&pscal_, nd * 32));
     ntt_ = std::make_unique<NttEngine>((int)h.log_domain, s0_);
-    // three engines on three streams: A/B1/C need only the witness and overlap the NTT;
-    // H follows the quotient on s0; the G2 MSM runs on s1
-    g1a_ = std::make_unique<MsmEngine>(Curve::G1, nv, s2_);
-    g1h_ = std::make_unique<MsmEngine>(Curve::G1, nd, s0_);
-    g2_ = std::make_unique<MsmEngine>(Curve::G2, nv, s1_);
+    // the witness plan (built on s2) feeds A/B1/C on s2 and B2 on s1; they overlap the
+    // quotient on s0, which then plans and runs the H MSM
+    plan_w_ = std::make_unique<MsmPlan>(nv, pw, s2_);
+    plan_h_ = std::make_unique<MsmPlan>(nd, ph, s0_);
+    g1a_ = std::make_unique<MsmEngine>(Curve::G1, pw, nv, s2_);
+    g2_ = std::make_unique<MsmEngine>(Curve::G2, pw, nv, s1_);
+    g1h_ = std::make_unique<MsmEngine>(Curve::G1, ph, nd, s0_);
     wina_ = g1a_->window_words();
     winh_ = g1h_->window_words();
     win2_ = g2_->window_words();
@@ -301,9 +351,16 @@ class DevicePipeline {
     g1a_.reset();
     g1h_.reset();
     g2_.reset();
-    for (void* p : {(void*)pa_, (void*)pb1_, (void*)pb2_, (void*)pc_, (void*)ph_, (void*)rowptr_[0], (void*)rowptr_[1],
-                    (void*)col_[0], (void*)col_[1], (void*)val_[0], (void*)val_[1], (void*)wit_, (void*)abc_[0],
-                    (void*)abc_[1], (void*)abc_[2], (void*)pscal_, (void*)dwin_})
+    plan_w_.reset();
+    plan_h_.reset();
+    ta_.reset();
+    tb1_.reset();
+    tc_.reset();
+    tb2_.reset();
+    th_.reset();
+    for (void* p : {(void*)rowptr_[0], (void*)rowptr_[1], (void*)col_[0], (void*)col_[1], (void*)val_[0],
+                    (void*)val_[1], (void*)wit_, (void*)abc_[0], (void*)abc_[1], (void*)abc_[2], (void*)pscal_,
+                    (void*)dwin_})
       if (p) (void)hipFree(p);
     for (uint32_t* p : slots_)
       if (p) (void)hipFree(p);
@@ -314,7 +371,6 @@ class DevicePipeline {
     (void)hipStreamDestroy(s2_);
   }
 
-  // enqueue witness upload + quotient (A4..A8); result scalars in pscal_
   // witness H2D into dst, bracketed by ev_[0]/ev_[1]
   void upload(const WtnsView& w, uint32_t* dst) {
     HIPX(hipEventRecord(ev_[0], s0_));
@@ -362,6 +418,13 @@ class DevicePipeline {
     g1 = stats_g1_;
     g2 = stats_g2_;
   }
+  void msm_params(MsmParams& pw, MsmParams& ph) const {
+    pw = plan_w_->params();
+    ph = plan_h_->params();
+  }
+  size_t table_bytes() const {
+    return ta_->bytes() + tb1_->bytes() + tc_->bytes() + tb2_->bytes() + th_->bytes();
+  }
 
   void quotient(const WtnsView& w, uint8_t* out) {
     std::lock_guard<std::mutex> lk(mu_);
@@ -397,62 +460,74 @@ class DevicePipeline {
   // the whole device pipeline on a resident witness (caller holds mu_, ev_[0..1] recorded)
   MsmOut prove_dev(const uint32_t* d_wit) {
     const ZkeyHeader& h = hdr_;
-    // window-sum layout in dwin_: A | B1 | C (engine g1a) | H (g1h) | B2 (g2)
+    // group-sum layout in dwin_: A | B1 | C (engine g1a) | H (g1h) | B2 (g2)
     uint32_t* wa = dwin_;
     uint32_t* wh = dwin_ + 3 * wina_;
     uint32_t* wb2 = wh + winh_;
-    // s1: G2 MSM (B2) and s2: G1 MSMs A, B1, C — both need only the resident witness.
-    // MsmEngine::run blocks its host thread once (the sort needs the nonzero-digit count),
-    // so each stream is fed from its own host thread; otherwise the host would serialise
-    // the streams at those syncs.
+    // s2: witness plan, then G1 MSMs A, B1, C;  s1: G2 MSM B2 on the same plan;
+    // s0: quotient (buildABC, 3 coset NTTs, joinABC), H plan, H MSM.
+    // MsmPlan::build blocks its host thread once (the sort needs the nonzero-digit
+    // count), so each stream is fed from its own host thread; the G2 thread starts
+    // once the witness plan is enqueued (its stream then waits on plan.ready()).
     // ZKP_SERIAL=1 (profiling only) chains the three streams so every kernel runs alone.
-    HIPX(hipStreamWaitEvent(s1_, ev_[1], 0));
     std::exception_ptr err[3];
-    auto g2_job = [&] {
-      try {
-        HIPX(hipSetDevice(dev_));
-        HIPX(hipEventRecord(ev_[7], s1_));
-        g2_->run(pb2_, d_wit, h.n_vars, wb2);
-        HIPX(hipEventRecord(ev_[6], s1_));
-      } catch (...) {
-        err[0] = std::current_exception();
-      }
-    };
+    std::promise<void> planned;
+    std::shared_future<void> planned_f = planned.get_future().share();
+    bool planned_set = false;
     auto g1_job = [&] {
       try {
         HIPX(hipSetDevice(dev_));
-        HIPX(hipStreamWaitEvent(s2_, serial_ ? ev_[6] : ev_[1], 0));
+        HIPX(hipStreamWaitEvent(s2_, ev_[1], 0));
         HIPX(hipEventRecord(ev_[9], s2_));
-        g1a_->run(pa_, d_wit, h.n_vars, wa);
-        g1a_->run(pb1_, d_wit, h.n_vars, wa + wina_);
-        g1a_->run(pc_, d_wit + (size_t)(h.n_public + 1) * 8, h.n_vars - h.n_public - 1, wa + 2 * wina_);
+        plan_w_->build(d_wit, h.n_vars);
+        planned.set_value();
+        planned_set = true;
+        g1a_->run(*plan_w_, *ta_, wa);
+        g1a_->run(*plan_w_, *tb1_, wa + wina_);
+        g1a_->run(*plan_w_, *tc_, wa + 2 * wina_);
         HIPX(hipEventRecord(ev_[8], s2_));
+      } catch (...) {
+        err[0] = std::current_exception();
+        if (!planned_set) planned.set_exception(std::current_exception());
+      }
+    };
+    auto g2_job = [&] {
+      try {
+        planned_f.get();
+        HIPX(hipSetDevice(dev_));
+        if (serial_) HIPX(hipStreamWaitEvent(s1_, ev_[8], 0));
+        HIPX(hipEventRecord(ev_[7], s1_));
+        g2_->run(*plan_w_, *tb2_, wb2);
+        HIPX(hipEventRecord(ev_[6], s1_));
       } catch (...) {
         err[1] = std::current_exception();
       }
     };
-    // s0: quotient (buildABC, 3 coset NTTs, joinABC) then the H MSM
     auto h_job = [&] {
       try {
-        if (serial_) HIPX(hipStreamWaitEvent(s0_, ev_[8], 0));
+        if (serial_) HIPX(hipStreamWaitEvent(s0_, ev_[6], 0));
         enqueue_quotient(d_wit);
-        g1h_->run(ph_, pscal_, h.domain_size, wh);
+        plan_h_->build(pscal_, h.domain_size);
+        g1h_->run(*plan_h_, *th_, wh);
       } catch (...) {
         err[2] = std::current_exception();
       }
     };
     if (serial_) {
-      g2_job();
-      if (!err[0]) g1_job();
+      g1_job();
+      if (!err[0]) g2_job();
       if (!err[0] && !err[1]) h_job();
     } else {
       std::thread t_g2(g2_job), t_g1(g1_job);
       h_job();
-      t_g2.join();
       t_g1.join();
+      t_g2.join();
     }
     for (auto& e : err)
-      if (e) std::rethrow_exception(e);
+      if (e) {
+        (void)hipDeviceSynchronize();  // let every enqueued kernel drain before buffers are reused
+        std::rethrow_exception(e);
+      }
     HIPX(hipEventRecord(ev_[4], s0_));
     HIPX(hipStreamWaitEvent(s0_, ev_[6], 0));
     HIPX(hipStreamWaitEvent(s0_, ev_[8], 0));
@@ -463,20 +538,19 @@ class DevicePipeline {
     g1h_->collect(stats_g1_);
     g2_->collect(stats_g2_);
     MsmOut o;
-    const int Wa = g1a_->params().windows, ca = g1a_->params().c;
-    const int Wh = g1h_->params().windows, ch = g1h_->params().c;
-    const int W2 = g2_->params().windows, c2 = g2_->params().c;
-    o.a = fold_windows<HFq>(hwin_, Wa, ca);
-    o.b1 = fold_windows<HFq>(hwin_ + wina_, Wa, ca);
-    o.c = fold_windows<HFq>(hwin_ + 2 * wina_, Wa, ca);
-    o.h = fold_windows<HFq>(hwin_ + 3 * wina_, Wh, ch);
-    o.b2 = fold_windows<HFq2>(hwin_ + 3 * wina_ + winh_, W2, c2);
+    const MsmParams& pa = g1a_->params();
+    const MsmParams& ph = g1h_->params();
+    o.a = msm_fold<HFq>(hwin_, pa);
+    o.b1 = msm_fold<HFq>(hwin_ + wina_, pa);
+    o.c = msm_fold<HFq>(hwin_ + 2 * wina_, pa);
+    o.h = msm_fold<HFq>(hwin_ + 3 * wina_, ph);
+    o.b2 = msm_fold<HFq2>(hwin_ + 3 * wina_ + winh_, pa);
     HIPX(hipEventElapsedTime(&o.ms[0], ev_[0], ev_[1]));  // wtns H2D
     HIPX(hipEventElapsedTime(&o.ms[1], ev_[1], ev_[2]));  // buildABC
     HIPX(hipEventElapsedTime(&o.ms[2], ev_[2], ev_[3]));  // NTT + join
-    HIPX(hipEventElapsedTime(&o.ms[3], ev_[9], ev_[8]));  // G1 MSMs A, B1, C (s2)
+    HIPX(hipEventElapsedTime(&o.ms[3], ev_[9], ev_[8]));  // witness plan + G1 MSMs A, B1, C (s2)
     HIPX(hipEventElapsedTime(&o.ms[4], ev_[7], ev_[6]));  // G2 MSM (s1)
-    HIPX(hipEventElapsedTime(&o.ms[5], ev_[3], ev_[4]));  // G1 MSM H (s0)
+    HIPX(hipEventElapsedTime(&o.ms[5], ev_[3], ev_[4]));  // H plan + G1 MSM H (s0)
     return o;
   }
 
@@ -486,7 +560,7 @@ class DevicePipeline {
   ZkeyHeader hdr_;
   hipStream_t s0_ = nullptr, s1_ = nullptr, s2_ = nullptr;
   hipEvent_t ev_[12];
-  uint32_t *pa_ = nullptr, *pb1_ = nullptr, *pb2_ = nullptr, *pc_ = nullptr, *ph_ = nullptr;
+  std::unique_ptr<MsmBases> ta_, tb1_, tc_, tb2_, th_;
   uint32_t* rowptr_[2] = {nullptr, nullptr};
   uint32_t* col_[2] = {nullptr, nullptr};
   uint32_t* val_[2] = {nullptr, nullptr};
@@ -494,6 +568,7 @@ class DevicePipeline {
   uint32_t* abc_[3] = {nullptr, nullptr, nullptr};
   uint32_t* pscal_ = nullptr;
   std::unique_ptr<NttEngine> ntt_;
+  std::unique_ptr<MsmPlan> plan_w_, plan_h_;
   std::unique_ptr<MsmEngine> g1a_, g1h_, g2_;
   size_t wina_ = 0, winh_ = 0, win2_ = 0;
   size_t win_total() const { return 3 * wina_ + winh_ + win2_; }
@@ -649,6 +724,14 @@ void Prover::set_instrument(bool on) {
   for (auto& d : devs_) d->set_instrument(on);
 }
 
+void Prover::msm_config(double* out, int n) const {
+  MsmParams pw, ph;
+  devs_[0]->msm_params(pw, ph);
+  const double v[7] = {(double)pw.c, (double)pw.depth, (double)pw.groups, (double)ph.c,
+                       (double)ph.depth, (double)ph.groups, (double)devs_[0]->table_bytes()};
+  for (int i = 0; i < n && i < 7; ++i) out[i] = v[i];
+}
+
 void Prover::kernel_stats(double* out, int n) const {
   MsmEngine::Stats a{}, b{};
   for (auto& d : devs_) {
@@ -664,30 +747,46 @@ void Prover::kernel_stats(double* out, int n) const {
 
 // ------------------------------------------------------------------ kernel-level helpers
 
-void msm_points(int device, Curve curve, const uint8_t* points, const uint8_t* scalars, size_t n, uint8_t* out,
-                int* is_inf) {
-  HIPX(hipSetDevice(device));
-  hipStream_t st;
-  HIPX(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-  const size_t pbytes = n * (curve == Curve::G1 ? 64 : 128);
-  uint32_t *dp = nullptr, *ds = nullptr, *dw = nullptr;
-  try {
-    MsmEngine eng(curve, std::max<size_t>(n, 1), st);
-    HIPX(hipMalloc(&dp, std::max<size_t>(pbytes, 64)));
-    HIPX(hipMalloc(&ds, std::max<size_t>(n * 32, 32)));
-    HIPX(hipMalloc(&dw, eng.window_words() * 4));
-    if (n) {
-      HIPX(hipMemcpyAsync(dp, points, pbytes, hipMemcpyHostToDevice, st));
-      HIPX(hipMemcpyAsync(ds, scalars, n * 32, hipMemcpyHostToDevice, st));
-      launch_convert_fq_zkey(dp, n * (curve == Curve::G1 ? 2 : 4), st);
+// One device-resident MSM set-up for the kernel-level entry points: base table from
+// zkey-layout points (row 0 uploaded + converted, rows 1..T-1 derived), a plan and an engine.
+struct MsmRig {
+  hipStream_t st = nullptr;
+  MsmParams prm;
+  std::unique_ptr<MsmBases> bases;
+  std::unique_ptr<MsmPlan> plan;
+  std::unique_ptr<MsmEngine> eng;
+  uint32_t *ds = nullptr, *dw = nullptr;
+  size_t n;
+  Curve curve;
+  MsmRig(int device, Curve cv, const uint8_t* points, const uint8_t* scalars, size_t n_, int c, int depth)
+      : n(n_), curve(cv) {
+    HIPX(hipSetDevice(device));
+    HIPX(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    try {
+      prm = MsmParams::make(std::max<size_t>(n, 1), c, depth);
+      bases = std::make_unique<MsmBases>(curve, n, prm.c, prm.depth);
+      fill_bases(*bases, points, n, 0, st);
+      plan = std::make_unique<MsmPlan>(std::max<size_t>(n, 1), prm, st);
+      eng = std::make_unique<MsmEngine>(curve, prm, std::max<size_t>(n, 1), st);
+      HIPX(hipMalloc(&ds, std::max<size_t>(n * 32, 32)));
+      HIPX(hipMalloc(&dw, eng->window_words() * 4));
+      if (n) HIPX(hipMemcpyAsync(ds, scalars, n * 32, hipMemcpyHostToDevice, st));
+    } catch (...) {
+      release();
+      throw;
     }
-    eng.run(dp, ds, n, dw);
-    std::vector<uint32_t> hw(eng.window_words());
+  }
+  void run() {
+    plan->build(ds, n);
+    eng->run(*plan, *bases, dw);
+  }
+  // fold the group sums and write the affine result (standard-form LE)
+  void result(uint8_t* out, int* is_inf) {
+    std::vector<uint32_t> hw(eng->window_words());
     HIPX(hipMemcpyAsync(hw.data(), dw, hw.size() * 4, hipMemcpyDeviceToHost, st));
     HIPX(hipStreamSynchronize(st));
-    const int W = eng.params().windows, c = eng.params().c;
     if (curve == Curve::G1) {
-      auto a = host::jac_to_aff(fold_windows<HFq>(hw.data(), W, c));
+      auto a = host::jac_to_aff(msm_fold<HFq>(hw.data(), prm));
       *is_inf = a.inf ? 1 : 0;
       std::memset(out, 0, 64);
       if (!a.inf) {
@@ -695,7 +794,7 @@ void msm_points(int device, Curve curve, const uint8_t* points, const uint8_t* s
         put_fq(a.y, out + 32);
       }
     } else {
-      auto a = host::jac_to_aff(fold_windows<HFq2>(hw.data(), W, c));
+      auto a = host::jac_to_aff(msm_fold<HFq2>(hw.data(), prm));
       *is_inf = a.inf ? 1 : 0;
       std::memset(out, 0, 128);
       if (!a.inf) {
@@ -705,84 +804,64 @@ void msm_points(int device, Curve curve, const uint8_t* points, const uint8_t* s
         put_fq(a.y.c1, out + 96);
       }
     }
-  } catch (...) {
-    for (void* p : {(void*)dp, (void*)ds, (void*)dw})
-      if (p) (void)hipFree(p);
-    (void)hipStreamDestroy(st);
-    throw;
   }
-  for (void* p : {(void*)dp, (void*)ds, (void*)dw})
-    if (p) (void)hipFree(p);
-  HIPX(hipStreamDestroy(st));
+  void release() {
+    if (st) (void)hipStreamSynchronize(st);
+    eng.reset();
+    plan.reset();
+    bases.reset();
+    for (void* p : {(void*)ds, (void*)dw})
+      if (p) (void)hipFree(p);
+    ds = dw = nullptr;
+    if (st) (void)hipStreamDestroy(st);
+    st = nullptr;
+  }
+  ~MsmRig() { release(); }
+};
+
+void msm_points(int device, Curve curve, const uint8_t* points, const uint8_t* scalars, size_t n, uint8_t* out,
+                int* is_inf, int c, int depth) {
+  MsmRig rig(device, curve, points, scalars, n, c, depth);
+  rig.run();
+  rig.result(out, is_inf);
 }
 
 MsmBench bench_msm(int device, Curve curve, const uint8_t* points, const uint8_t* scalars, size_t n, int warmup,
                    int iters, uint8_t* out, int* is_inf) {
   if (n == 0 || iters <= 0) throw ZkpError(ZKP_ERR_INVALID_ARG, "bench_msm: n and iters must be > 0");
-  HIPX(hipSetDevice(device));
-  hipStream_t st;
-  HIPX(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-  const size_t pbytes = n * (curve == Curve::G1 ? 64 : 128);
-  uint32_t *dp = nullptr, *ds = nullptr, *dw = nullptr;
+  MsmRig rig(device, curve, points, scalars, n, 0, 0);
   hipEvent_t e0, e1;
   HIPX(hipEventCreate(&e0));
   HIPX(hipEventCreate(&e1));
   MsmBench r;
   try {
-    MsmEngine eng(curve, n, st);
-    HIPX(hipMalloc(&dp, pbytes));
-    HIPX(hipMalloc(&ds, n * 32));
-    HIPX(hipMalloc(&dw, eng.window_words() * 4));
-    HIPX(hipMemcpyAsync(dp, points, pbytes, hipMemcpyHostToDevice, st));
-    HIPX(hipMemcpyAsync(ds, scalars, n * 32, hipMemcpyHostToDevice, st));
-    launch_convert_fq_zkey(dp, n * (curve == Curve::G1 ? 2 : 4), st);
-    for (int i = 0; i < warmup; ++i) eng.run(dp, ds, n, dw);
-    HIPX(hipStreamSynchronize(st));
-    // pass 1: whole-pipeline time, nothing but the MSM launches between the events
-    HIPX(hipEventRecord(e0, st));
-    for (int i = 0; i < iters; ++i) eng.run(dp, ds, n, dw);
-    HIPX(hipEventRecord(e1, st));
+    for (int i = 0; i < warmup; ++i) rig.run();
+    HIPX(hipStreamSynchronize(rig.st));
+    // pass 1: whole-pipeline time (plan + engine), host-blocking once per MSM as in a proof
+    HIPX(hipEventRecord(e0, rig.st));
+    for (int i = 0; i < iters; ++i) rig.run();
+    HIPX(hipEventRecord(e1, rig.st));
     HIPX(hipEventSynchronize(e1));
     float ms = 0;
     HIPX(hipEventElapsedTime(&ms, e0, e1));
     r.ms_per_msm = ms / iters;
     // pass 2: per-launch events around the bucket-accumulate kernel
-    eng.set_instrument(true);
+    rig.eng->set_instrument(true);
     MsmEngine::Stats s;
-    for (int i = 0; i < std::min(iters, 8); ++i) eng.run(dp, ds, n, dw);
-    HIPX(hipStreamSynchronize(st));
-    eng.collect(s);
+    for (int i = 0; i < std::min(iters, 8); ++i) rig.run();
+    HIPX(hipStreamSynchronize(rig.st));
+    rig.eng->collect(s);
     r.ms_accumulate = (float)(s.accumulate_ms / std::max<uint64_t>(1, s.launches));
     r.mixed_adds = s.mixed_adds / std::max<uint64_t>(1, s.launches);
     r.tasks = s.tasks / std::max<uint64_t>(1, s.launches);
-    r.c = eng.params().c;
-    r.windows = eng.params().windows;
-    std::vector<uint32_t> hw(eng.window_words());
-    HIPX(hipMemcpyAsync(hw.data(), dw, hw.size() * 4, hipMemcpyDeviceToHost, st));
-    HIPX(hipStreamSynchronize(st));
-    if (out && is_inf) {
-      if (curve == Curve::G1) {
-        auto a = host::jac_to_aff(fold_windows<HFq>(hw.data(), r.windows, r.c));
-        *is_inf = a.inf;
-        std::memset(out, 0, 64);
-        if (!a.inf) put_fq(a.x, out), put_fq(a.y, out + 32);
-      } else {
-        auto a = host::jac_to_aff(fold_windows<HFq2>(hw.data(), r.windows, r.c));
-        *is_inf = a.inf;
-        std::memset(out, 0, 128);
-        if (!a.inf) put_fq(a.x.c0, out), put_fq(a.x.c1, out + 32), put_fq(a.y.c0, out + 64), put_fq(a.y.c1, out + 96);
-      }
-    }
+    r.c = rig.prm.c;
+    r.windows = rig.prm.windows;
+    if (out && is_inf) rig.result(out, is_inf);
   } catch (...) {
-    for (void* p : {(void*)dp, (void*)ds, (void*)dw})
-      if (p) (void)hipFree(p);
-    (void)hipEventDestroy(e0), (void)hipEventDestroy(e1), (void)hipStreamDestroy(st);
+    (void)hipEventDestroy(e0), (void)hipEventDestroy(e1);
     throw;
   }
-  for (void* p : {(void*)dp, (void*)ds, (void*)dw})
-    if (p) (void)hipFree(p);
   (void)hipEventDestroy(e0), (void)hipEventDestroy(e1);
-  HIPX(hipStreamDestroy(st));
   return r;
 }
 

@@ -78,6 +78,9 @@ class Prover {
   void set_instrument(bool on);
   void kernel_stats(double* out, int n) const;
   int device_count() const { return (int)devs_.size(); }
+  // MSM configuration of device 0: [0] witness c, [1] witness depth, [2] witness groups,
+  // [3] H c, [4] H depth, [5] H groups, [6] base-table bytes per device
+  void msm_config(double* out, int n) const;
 
  private:
   ZkeyHeader hdr_;
@@ -91,8 +94,9 @@ class Prover {
 };
 
 // kernel-level helpers (C-ABI zkp_msm_g1/g2, zkp_ntt_fr)
+// c / depth: window bits and base-table depth (0 = automatic, as the prover)
 void msm_points(int device, Curve curve, const uint8_t* points, const uint8_t* scalars, size_t n, uint8_t* out,
-                int* is_inf);
+                int* is_inf, int c = 0, int depth = 0);
 void ntt_fr(int device, uint8_t* data, size_t n, int mode);
 // device-resident kernel benchmarks (HIP events on the engine stream)
 struct MsmBench {

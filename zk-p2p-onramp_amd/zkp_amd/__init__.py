@@ -99,11 +99,14 @@ def load_library(path: str = LIB_PATH):
                                       ctypes.POINTER(ctypes.c_double), u8p, ctypes.POINTER(ctypes.c_int)]
         lib.zkp_bench_ntt.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                       ctypes.POINTER(ctypes.c_double)]
+        lib.zkp_msm.argtypes = [ctypes.c_int, ctypes.c_int, u8p, u8p, sz, ctypes.c_int, ctypes.c_int, u8p,
+                                ctypes.POINTER(ctypes.c_int)]
+        lib.zkp_prover_msm_config.argtypes = [P, ctypes.POINTER(ctypes.c_double), ctypes.c_int]
         for name in ("zkp_prover_load_mem", "zkp_prover_load_file", "zkp_prover_info", "zkp_prove",
                      "zkp_prove_batch", "zkp_prove_files", "zkp_proof_json", "zkp_public_json",
                      "zkp_prover_timings", "zkp_msm_g1", "zkp_msm_g2", "zkp_ntt_fr", "zkp_quotient",
                      "zkp_witness_stage", "zkp_prove_staged", "zkp_prover_instrument", "zkp_prover_kernel_stats",
-                     "zkp_bench_msm", "zkp_bench_ntt"):
+                     "zkp_bench_msm", "zkp_bench_ntt", "zkp_msm", "zkp_prover_msm_config"):
             getattr(lib, name).restype = ctypes.c_int
         _lib = lib
         return lib
@@ -253,6 +256,14 @@ class Prover:
     def instrument(self, on: bool = True):
         _check(load_library().zkp_prover_instrument(self._h, 1 if on else 0))
 
+    def msm_config(self):
+        out = (ctypes.c_double * 7)()
+        _check(load_library().zkp_prover_msm_config(self._h, out, 7))
+        v = list(out)
+        return {"witness": {"c": int(v[0]), "depth": int(v[1]), "groups": int(v[2])},
+                "h": {"c": int(v[3]), "depth": int(v[4]), "groups": int(v[5])},
+                "table_bytes_per_device": int(v[6])}
+
     def kernel_stats(self):
         out = (ctypes.c_double * 8)()
         _check(load_library().zkp_prover_kernel_stats(self._h, out, 8))
@@ -322,34 +333,36 @@ class _Groth16:
 groth16 = _Groth16()
 
 
-def msm_g1(points_lem: bytes, scalars_le: bytes, device: int = 0):
-    """Kernel-level G1 MSM: zkey-layout points, 32-byte LE scalars -> affine (x, y) or None."""
-    lib = load_library()
-    n = len(scalars_le) // 32
-    pp, pk = _buf(points_lem)
-    sp, sk = _buf(scalars_le)
-    out = (ctypes.c_uint8 * 64)()
-    inf = ctypes.c_int()
-    _check(lib.zkp_msm_g1(device, pp, sp, n, ctypes.cast(out, ctypes.POINTER(ctypes.c_uint8)), ctypes.byref(inf)))
-    if inf.value:
-        return None
-    raw = bytes(out)
-    return (_le(raw[:32]), _le(raw[32:]))
-
-
-def msm_g2(points_lem: bytes, scalars_le: bytes, device: int = 0):
+def _msm(points_lem, scalars_le, g2, device, window_bits, table_depth):
     lib = load_library()
     n = len(scalars_le) // 32
     pp, pk = _buf(points_lem)
     sp, sk = _buf(scalars_le)
     out = (ctypes.c_uint8 * 128)()
     inf = ctypes.c_int()
-    _check(lib.zkp_msm_g2(device, pp, sp, n, ctypes.cast(out, ctypes.POINTER(ctypes.c_uint8)), ctypes.byref(inf)))
+    o = ctypes.cast(out, ctypes.POINTER(ctypes.c_uint8))
+    if window_bits or table_depth:
+        _check(lib.zkp_msm(device, 1 if g2 else 0, pp, sp, n, window_bits, table_depth, o, ctypes.byref(inf)))
+    elif g2:
+        _check(lib.zkp_msm_g2(device, pp, sp, n, o, ctypes.byref(inf)))
+    else:
+        _check(lib.zkp_msm_g1(device, pp, sp, n, o, ctypes.byref(inf)))
     if inf.value:
         return None
     raw = bytes(out)
     v = [_le(raw[32 * i:32 * i + 32]) for i in range(4)]
-    return ((v[0], v[1]), (v[2], v[3]))
+    return ((v[0], v[1]), (v[2], v[3])) if g2 else (v[0], v[1])
+
+
+def msm_g1(points_lem: bytes, scalars_le: bytes, device: int = 0, window_bits: int = 0, table_depth: int = 0):
+    """Kernel-level G1 MSM: zkey-layout points, 32-byte LE scalars -> affine (x, y) or None.
+    window_bits / table_depth: Pippenger parameters (0 = automatic, as the prover)."""
+    return _msm(points_lem, scalars_le, False, device, window_bits, table_depth)
+
+
+def msm_g2(points_lem: bytes, scalars_le: bytes, device: int = 0, window_bits: int = 0, table_depth: int = 0):
+    """Kernel-level G2 MSM -> ((x.c0, x.c1), (y.c0, y.c1)) or None."""
+    return _msm(points_lem, scalars_le, True, device, window_bits, table_depth)
 
 
 def ntt_fr(values, mode: int, device: int = 0):
