@@ -57,11 +57,26 @@ typedef struct zkp_proof {
   uint8_t* public_signals;
 } zkp_proof;
 
+/* MSM partial sums of one point range of one proof (the point-range split of a single
+ * proof over several GPUs).  Affine standard-form LE, all-zero =
+ * infinity.  392 bytes, no padding: ranks exchange these by an RCCL all-gather. */
+typedef struct zkp_partial {
+  uint8_t a[64], b1[64], c[64], h[64]; /* G1: sum over the slice of w_i A_i, w_i B1_i, w_i C_i, P_j H_j */
+  uint8_t b2[128];                     /* G2: sum over the slice of w_i B2_i                          */
+  uint32_t part, nparts;
+} zkp_partial;
+
 /* Load a .zkey (snarkjs groth16, version 1) from a path or a memory buffer.
  * devices: HIP device ordinals (NULL/0 -> device 0).  Every device gets a full
  * resident copy (batch mode: proofs are spread over devices by zkp_prove_batch). */
 zkp_status zkp_prover_load_file(const char* zkey_path, const int* devices, int ndev, zkp_prover** out);
 zkp_status zkp_prover_load_mem(const uint8_t* zkey, size_t len, const int* devices, int ndev, zkp_prover** out);
+
+/* Load only point slice `part` of `nparts` (contiguous ranges of the witness-indexed
+ * sections 5-8 and of section 9) onto one device.  Such a prover computes partial sums
+ * only (zkp_prove_partial); the quotient is computed in full on every part. */
+zkp_status zkp_prover_load_part(const uint8_t* zkey, size_t len, int device, int part, int nparts,
+                                zkp_prover** out);
 
 zkp_status zkp_prover_info(const zkp_prover* p, uint32_t* n_vars, uint32_t* n_public, uint32_t* domain_size);
 
@@ -75,6 +90,16 @@ zkp_status zkp_prove(zkp_prover* p, const uint8_t* wtns, size_t len, const uint8
  * r32s / s32s may be NULL (all random) or arrays of n pointers. */
 zkp_status zkp_prove_batch(zkp_prover* p, const uint8_t* const* wtns, const size_t* lens, int n,
                            const uint8_t* const* r32s, const uint8_t* const* s32s, zkp_proof* outs);
+
+/* Partial MSM sums of this prover's slice for one witness (any prover; a full one
+ * reports part 0 of 1). */
+zkp_status zkp_prove_partial(zkp_prover* p, const uint8_t* wtns, size_t len, zkp_partial* out);
+/* Host only (no device): sum the nparts partials of one split, then blind (r32 / s32 as
+ * in zkp_prove) and assemble the proof; public signals come from wtns.  The result is
+ * bit-identical to zkp_prove on the full key. */
+zkp_status zkp_proof_combine(const uint8_t* zkey, size_t len, const zkp_partial* parts, int nparts,
+                             const uint8_t* wtns, size_t wlen, const uint8_t* r32, const uint8_t* s32,
+                             zkp_proof* out);
 
 /* CLI-equivalent: `groth16 prove <zkey> <wtns> <proof.json> <public.json>` on a
  * loaded prover; writes JSON byte-compatible with snarkjs (JSON.stringify(x,null,1)). */
@@ -126,6 +151,7 @@ zkp_status zkp_quotient(zkp_prover* p, const uint8_t* wtns, size_t len, uint8_t*
 zkp_status zkp_witness_stage(zkp_prover* p, int dev_index, int slot, const uint8_t* wtns, size_t len);
 zkp_status zkp_prove_staged(zkp_prover* p, int dev_index, int slot, const uint8_t* r32, const uint8_t* s32,
                             zkp_proof* out);
+zkp_status zkp_prove_partial_staged(zkp_prover* p, int slot, zkp_partial* out);
 /* Bracket every bucket-accumulate kernel launch with HIP events (on its stream).
  * zkp_prover_kernel_stats: [0] G1 accumulate ms (sum), [1] G1 launches, [2] G1 mixed
  * additions, [3] G1 tasks, [4..7] the same for G2.  Enabling resets the counters. */

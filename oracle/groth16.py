@@ -88,6 +88,32 @@ def prove(z: ZKey, w, r: int, s: int):
     return {"A": A, "B": B, "C": C}, w[1:z.n_public + 1]
 
 
+def split_range(n: int, part: int, nparts: int):
+    """[lo, hi) of slice `part` of n items in nparts contiguous ranges (as prover.hip split_range)."""
+    return n * part // nparts, n * (part + 1) // nparts
+
+
+def partial_sums(z: ZKey, w, part: int, nparts: int, h=None):
+    """MSM partial sums of point slice `part` of `nparts` (the point-range split of one proof,
+    SURVEY.md §8e E1(2)): witness-indexed sections A, B1, B2, C over [wlo, whi) (C's base of
+    signal i is z.c[i - nPublic - 1]), H over [hlo, hhi) of the domain.  Summing the partials
+    of all parts gives prove()'s pa, pb1, pb, pc, ph."""
+    w = [x % R for x in w]
+    if h is None:
+        h = quotient_scalars(z, w)
+    wlo, whi = split_range(z.n_vars, part, nparts)
+    hlo, hhi = split_range(z.domain_size, part, nparts)
+    c0 = z.n_public + 1
+    cidx = [i for i in range(max(wlo, c0), whi)]
+    return {
+        "a": msm_g1(z.a[wlo:whi], w[wlo:whi]),
+        "b1": msm_g1(z.b1[wlo:whi], w[wlo:whi]),
+        "c": msm_g1([z.c[i - c0] for i in cidx], [w[i] for i in cidx]),
+        "h": msm_g1(z.h[hlo:hhi], h[hlo:hhi]),
+        "b2": msm_g2(z.b2[wlo:whi], w[wlo:whi]),
+    }
+
+
 def verify(vk_ic, alpha1, beta2, gamma2, delta2, public, proof) -> bool:
     if len(public) + 1 != len(vk_ic):
         raise ValueError("verifier-bad-input")

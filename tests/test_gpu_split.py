@@ -1,0 +1,34 @@
+"""GPU parity of the point-range split of one proof: every
+slice's partial sums equal the oracle's bit-exactly, and combining them gives the
+golden proof."""
+import pytest
+
+import zkp_amd
+from test_split import _case, _oracle_partials
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("name,nparts", [("tiny", 4), ("small", 2), ("small", 3), ("venmo_mini", 5)])
+def test_split_partials_bit_exact_and_combine(name, nparts):
+    zk, wt, r, s, want = _case(name)
+    parts = []
+    for k in range(nparts):
+        p = zkp_amd.Prover(zk, devices=[0], part=k, nparts=nparts)
+        parts.append(p.prove_partial(wt))
+        with pytest.raises(zkp_amd.ZkpError):  # a slice cannot make a full proof
+            p.prove_raw(wt, r, s)
+        p.close()
+    assert parts == _oracle_partials(zk, wt, nparts)
+    (a, b, c), _ = zkp_amd.proof_combine_raw(zk, parts, wt, r, s)
+    assert {"A": a, "B": b, "C": c} == want
+
+
+def test_full_prover_partial_is_part_0_of_1():
+    zk, wt, r, s, want = _case("small")
+    p = zkp_amd.Prover(zk)
+    part = p.prove_partial(wt)
+    assert part[-8:] == (0).to_bytes(4, "little") + (1).to_bytes(4, "little")
+    (a, b, c), _ = zkp_amd.proof_combine_raw(zk, [part], wt, r, s)
+    assert {"A": a, "B": b, "C": c} == want
+    assert p.prove_raw(wt, r, s)[0] == (a, b, c)

@@ -1,0 +1,97 @@
+"""Point-range split of ONE proof over several GPUs (SURVEY.md §8e E1(2), configs[4]):
+host-side combine + the all-gather transport, without a GPU.
+
+Partials here come from the oracle's restatement of the split (oracle.groth16.partial_sums);
+zkp_proof_combine (host C code in libzkp_amd.so, no device) must turn any complete set
+of them into the golden proof bit-exactly, and the gloo all-gather (world_size 2, the
+same code path that runs over RCCL/xGMI with backend "nccl") must deliver them."""
+import json
+import os
+import random
+import socket
+
+import pytest
+import torch.multiprocessing as mp
+
+from oracle import binfile, groth16
+import zkp_amd
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLD = os.path.join(ROOT, "tests", "golden")
+
+
+def _case(name):
+    zk = open(os.path.join(GOLD, "circuit_%s.zkey" % name), "rb").read()
+    wt = open(os.path.join(GOLD, "circuit_%s.wtns" % name), "rb").read()
+    man = json.load(open(os.path.join(GOLD, "manifest.json")))["circuits"][name]
+    want = groth16.proof_from_json_obj(json.load(open(os.path.join(GOLD, "proof_%s.json" % name))))
+    return zk, wt, int(man["r"]), int(man["s"]), want
+
+
+def _oracle_partials(zk, wt, nparts):
+    z = binfile.read_zkey(zk)
+    w = binfile.read_wtns(wt)[1]
+    h = groth16.quotient_scalars(z, [x % groth16.R for x in w])
+    out = []
+    for k in range(nparts):
+        p = groth16.partial_sums(z, w, k, nparts, h)
+        out.append(zkp_amd.partial_from_points(p["a"], p["b1"], p["c"], p["h"], p["b2"], k, nparts))
+    return out
+
+
+@pytest.mark.parametrize("name,nparts", [("tiny", 1), ("tiny", 3), ("small", 2), ("small", 7)])
+def test_combine_oracle_partials_is_golden(name, nparts):
+    zk, wt, r, s, want = _case(name)
+    parts = _oracle_partials(zk, wt, nparts)
+    random.Random(nparts).shuffle(parts)  # any order
+    (a, b, c), pub = zkp_amd.proof_combine_raw(zk, parts, wt, r, s)
+    assert {"A": a, "B": b, "C": c} == want
+    assert pub == [x % groth16.R for x in binfile.read_wtns(wt)[1][1:len(pub) + 1]]
+
+
+def test_combine_rejects_incomplete_or_duplicate_parts():
+    zk, wt, r, s, _ = _case("tiny")
+    parts = _oracle_partials(zk, wt, 3)
+    for bad in (parts[:2], [parts[0], parts[0], parts[2]]):
+        with pytest.raises(zkp_amd.ZkpError) as e:
+            zkp_amd.proof_combine_raw(zk, bad, wt, r, s)
+        assert e.value.status == 1
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, name, q):
+    import torch.distributed as dist
+    from zkp_amd.dist import all_gather_partials
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        zk, wt, r, s, _ = _case(name)
+        mine = _oracle_partials(zk, wt, world)[rank]  # rank k computes slice k only
+        parts = all_gather_partials(mine, None)
+        (a, b, c), _ = zkp_amd.proof_combine_raw(zk, parts, wt, r, s)
+        q.put((rank, [p[-8:] for p in parts], (a, b, c)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_split_allgather_gloo_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(k, 2, port, "tiny", q)) for k in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    _, _, _, _, want = _case("tiny")
+    for rank, tags, (a, b, c) in res:
+        assert tags == [k.to_bytes(4, "little") + (2).to_bytes(4, "little") for k in range(2)]  # rank order
+        assert {"A": a, "B": b, "C": c} == want

@@ -14,6 +14,8 @@
 #include "host_ec.hpp"
 #include "prover.hpp"
 
+static_assert(sizeof(zkp_partial) == 392, "zkp_partial is exchanged as 392 raw bytes");
+
 struct zkp_prover {
   zkp::Prover* impl;
 };
@@ -129,6 +131,39 @@ zkp_status zkp_prover_load_file(const char* path, const int* devices, int ndev, 
   zkp_status s = guard([&] { buf = read_file(path); });
   if (s != ZKP_OK) return s;
   return zkp_prover_load_mem(buf.data(), buf.size(), devices, ndev, out);
+}
+
+zkp_status zkp_prover_load_part(const uint8_t* zkey, size_t len, int device, int part, int nparts,
+                                zkp_prover** out) {
+  if (!zkey || !out) return fail(ZKP_ERR_INVALID_ARG, "null argument");
+  *out = nullptr;
+  return guard([&] {
+    auto* h = new zkp_prover{nullptr};
+    try {
+      h->impl = new zkp::Prover(zkey, len, std::vector<int>{device}, part, nparts);
+    } catch (...) {
+      delete h;
+      throw;
+    }
+    *out = h;
+  });
+}
+
+zkp_status zkp_prove_partial(zkp_prover* p, const uint8_t* wtns, size_t len, zkp_partial* out) {
+  if (!p || !wtns || !out) return fail(ZKP_ERR_INVALID_ARG, "null argument");
+  return guard([&] { p->impl->prove_partial(wtns, len, out); });
+}
+
+zkp_status zkp_prove_partial_staged(zkp_prover* p, int slot, zkp_partial* out) {
+  if (!p || !out) return fail(ZKP_ERR_INVALID_ARG, "null argument");
+  return guard([&] { p->impl->prove_partial_staged(slot, out); });
+}
+
+zkp_status zkp_proof_combine(const uint8_t* zkey, size_t len, const zkp_partial* parts, int nparts,
+                             const uint8_t* wtns, size_t wlen, const uint8_t* r32, const uint8_t* s32,
+                             zkp_proof* out) {
+  if (!zkey || !parts || !wtns || !out || nparts < 1) return fail(ZKP_ERR_INVALID_ARG, "bad argument");
+  return guard([&] { zkp::proof_combine(zkey, len, parts, nparts, wtns, wlen, r32, s32, out); });
 }
 
 zkp_status zkp_prover_info(const zkp_prover* p, uint32_t* n_vars, uint32_t* n_public, uint32_t* domain_size) {

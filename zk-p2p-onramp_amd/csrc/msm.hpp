@@ -59,7 +59,7 @@ struct MsmParams {
     // one bucket set of 2^(c-1) buckets against n*W entries: c = lg - 3 keeps every
     // bucket ~16*W entries deep and the bucket reduction (2^c full adds) < 2% of the
     // accumulation; 20 bits caps the sort at three 8-bit passes.
-    p.c = c_override > 0 ? c_override : (lg - 3 < 8 ? 8 : (lg - 3 > 20 ? 20 : lg - 3));
+    p.c = c_override > 0 ? c_override : (lg - 4 < 8 ? 8 : (lg - 4 > 20 ? 20 : lg - 4));
     if (p.c < 2) p.c = 2;
     if (p.c > 24) p.c = 24;
     p.windows = (255 + p.c - 1) / p.c;

@@ -103,7 +103,7 @@ struct ZkeyParsed {
   Csr csr[2];
 };
 
-static ZkeyParsed parse_zkey(const uint8_t* buf, size_t len) {
+static ZkeyParsed parse_zkey(const uint8_t* buf, size_t len, bool with_coefs = true) {
   ZkeyParsed z;
   z.bf = parse_binfile(buf, len, "zkey", 1);
   const Section& s1 = z.bf.sec[1];
@@ -157,6 +157,7 @@ static ZkeyParsed parse_zkey(const uint8_t* buf, size_t len) {
   if (!s4.ptr || s4.len < 4) throw ZkpError(ZKP_ERR_FORMAT, "zkey: missing coefficients section");
   h.n_coef = rd32(s4.ptr);
   if (s4.len != 4 + (uint64_t)h.n_coef * 44) throw ZkpError(ZKP_ERR_FORMAT, "zkey: coefficients section has an invalid size");
+  if (!with_coefs) return z;
   // CSR by (matrix, constraint) with a stable counting sort
   for (int m = 0; m < 2; ++m) z.csr[m].rowptr.assign((size_t)h.domain_size + 1, 0);
   const uint8_t* c = s4.ptr + 4;
@@ -286,9 +287,17 @@ static void fill_bases(MsmBases& b, const uint8_t* src, size_t count, size_t at,
   b.extend(st);
 }
 
+// [lo, hi) of slice `part` when n items are cut into nparts contiguous ranges
+static void split_range(size_t n, int part, int nparts, size_t& lo, size_t& hi) {
+  lo = n * (size_t)part / (size_t)nparts;
+  hi = n * (size_t)(part + 1) / (size_t)nparts;
+}
+
 class DevicePipeline {
  public:
-  DevicePipeline(int dev, const ZkeyParsed& z) : dev_(dev), hdr_(z.hdr) {
+  // part / nparts: this pipeline holds only slice `part` of every point section (the
+  // point-range split of one proof over several GPUs); 0 / 1 = all
+  DevicePipeline(int dev, const ZkeyParsed& z, int part = 0, int nparts = 1) : dev_(dev), hdr_(z.hdr) {
     HIPX(hipSetDevice(dev_));
     // s0 carries the critical path (quotient -> H plan -> H MSM): highest priority, so the
     // A/B1/C (s2) and B2 (s1) MSMs fill the CUs it leaves idle instead of delaying it
@@ -299,7 +308,10 @@ class DevicePipeline {
     HIPX(hipStreamCreateWithPriority(&s2_, hipStreamNonBlocking, prio_lo));
     for (auto& e : ev_) HIPX(hipEventCreate(&e));
     const ZkeyHeader& h = hdr_;
-    const size_t nv = h.n_vars, nd = h.domain_size, nc = h.n_vars - h.n_public - 1;
+    const size_t nd_all = h.domain_size, c0 = (size_t)h.n_public + 1;  // first witness index with a C base
+    split_range(h.n_vars, part, nparts, wlo_, whi_);
+    split_range(h.domain_size, part, nparts, hlo_, hhi_);
+    const size_t nv = whi_ - wlo_, nd = hhi_ - hlo_;
     MsmParams pw, ph;
     choose_msm_params(nv, nd, pw, ph);
     // base tables: A, B1, C, B2 indexed by witness signal (C's first nPublic+1 bases are
@@ -309,11 +321,16 @@ class DevicePipeline {
     tc_ = std::make_unique<MsmBases>(Curve::G1, nv, pw.c, pw.depth);
     tb2_ = std::make_unique<MsmBases>(Curve::G2, nv, pw.c, pw.depth);
     th_ = std::make_unique<MsmBases>(Curve::G1, nd, ph.c, ph.depth);
-    fill_bases(*ta_, z.bf.sec[5].ptr, nv, 0, s0_);
-    fill_bases(*tb1_, z.bf.sec[6].ptr, nv, 0, s0_);
-    fill_bases(*tb2_, z.bf.sec[7].ptr, nv, 0, s0_);
-    fill_bases(*tc_, z.bf.sec[8].ptr, nc, nv - nc, s0_);
-    fill_bases(*th_, z.bf.sec[9].ptr, nd, 0, s0_);
+    fill_bases(*ta_, z.bf.sec[5].ptr + wlo_ * 64, nv, 0, s0_);
+    fill_bases(*tb1_, z.bf.sec[6].ptr + wlo_ * 64, nv, 0, s0_);
+    fill_bases(*tb2_, z.bf.sec[7].ptr + wlo_ * 128, nv, 0, s0_);
+    {
+      const size_t cfirst = std::max(wlo_, c0);  // first witness index of the slice with a C base
+      const size_t lead = std::min(cfirst, whi_) - wlo_;
+      const size_t cnt = whi_ > cfirst ? whi_ - cfirst : 0;
+      fill_bases(*tc_, cnt ? z.bf.sec[8].ptr + (cfirst - c0) * 64 : nullptr, cnt, lead, s0_);
+    }
+    fill_bases(*th_, z.bf.sec[9].ptr + hlo_ * 64, nd, 0, s0_);
     for (int m = 0; m < 2; ++m) {
       const Csr& c = z.csr[m];
       HIPX(hipMalloc(&rowptr_[m], c.rowptr.size() * 4));
@@ -326,9 +343,9 @@ class DevicePipeline {
         launch_convert_coefs(val_[m], c.col.size(), s0_);
       }
     }
-    HIPX(hipMalloc(&wit_, std::max<size_t>(nv * 32, 32)));
-    for (auto& b : abc_) HIPX(hipMalloc(&b, nd * 32));
-    HIPX(hipMalloc(&pscal_, nd * 32));
+    HIPX(hipMalloc(&wit_, std::max<size_t>((size_t)h.n_vars * 32, 32)));
+    for (auto& b : abc_) HIPX(hipMalloc(&b, nd_all * 32));
+    HIPX(hipMalloc(&pscal_, nd_all * 32));
     ntt_ = std::make_unique<NttEngine>((int)h.log_domain, s0_);
     // the witness plan (built on s2) feeds A/B1/C on s2 and B2 on s1; they overlap the
     // quotient on s0, which then plans and runs the H MSM
@@ -479,7 +496,7 @@ class DevicePipeline {
         HIPX(hipSetDevice(dev_));
         HIPX(hipStreamWaitEvent(s2_, ev_[1], 0));
         HIPX(hipEventRecord(ev_[9], s2_));
-        plan_w_->build(d_wit, h.n_vars);
+        plan_w_->build(d_wit + wlo_ * 8, whi_ - wlo_);
         planned.set_value();
         planned_set = true;
         g1a_->run(*plan_w_, *ta_, wa);
@@ -507,7 +524,7 @@ class DevicePipeline {
       try {
         if (serial_) HIPX(hipStreamWaitEvent(s0_, ev_[6], 0));
         enqueue_quotient(d_wit);
-        plan_h_->build(pscal_, h.domain_size);
+        plan_h_->build(pscal_ + hlo_ * 8, hhi_ - hlo_);
         g1h_->run(*plan_h_, *th_, wh);
       } catch (...) {
         err[2] = std::current_exception();
@@ -556,6 +573,7 @@ class DevicePipeline {
 
  private:
   int dev_;
+  size_t wlo_ = 0, whi_ = 0, hlo_ = 0, hhi_ = 0;  // witness / domain slice held by this pipeline
   bool serial_ = std::getenv("ZKP_SERIAL") && std::getenv("ZKP_SERIAL")[0] == '1';  // profiling: no stream overlap
   ZkeyHeader hdr_;
   hipStream_t s0_ = nullptr, s1_ = nullptr, s2_ = nullptr;
@@ -581,7 +599,10 @@ class DevicePipeline {
 
 // ------------------------------------------------------------------ Prover
 
-Prover::Prover(const uint8_t* zkey, size_t len, const std::vector<int>& devices) {
+Prover::Prover(const uint8_t* zkey, size_t len, const std::vector<int>& devices, int part, int nparts)
+    : part_(part), nparts_(nparts) {
+  if (nparts < 1 || part < 0 || part >= nparts) throw ZkpError(ZKP_ERR_INVALID_ARG, "bad part / nparts");
+  if (nparts > 1 && devices.size() > 1) throw ZkpError(ZKP_ERR_INVALID_ARG, "a partial prover runs on one device");
   ZkeyParsed z = parse_zkey(zkey, len);
   hdr_ = z.hdr;
   int ndev = 0;
@@ -590,7 +611,7 @@ Prover::Prover(const uint8_t* zkey, size_t len, const std::vector<int>& devices)
   std::vector<int> devs = devices.empty() ? std::vector<int>{0} : devices;
   for (int d : devs) {
     if (d < 0 || d >= ndev) throw ZkpError(ZKP_ERR_INVALID_ARG, "device ordinal out of range");
-    devs_.push_back(std::make_unique<DevicePipeline>(d, z));
+    devs_.push_back(std::make_unique<DevicePipeline>(d, z, part, nparts));
   }
 }
 
@@ -638,7 +659,92 @@ static WtnsView check_wtns(const ZkeyHeader& h, const uint8_t* wtns, size_t len)
   return w;
 }
 
+static void jac_to_bytes_g1(const Jac<HFq>& p, uint8_t* out) {
+  std::memset(out, 0, 64);
+  auto a = host::jac_to_aff(p);
+  if (!a.inf) put_fq(a.x, out), put_fq(a.y, out + 32);
+}
+static void jac_to_bytes_g2(const Jac<HFq2>& p, uint8_t* out) {
+  std::memset(out, 0, 128);
+  auto a = host::jac_to_aff(p);
+  if (!a.inf) put_fq(a.x.c0, out), put_fq(a.x.c1, out + 32), put_fq(a.y.c0, out + 64), put_fq(a.y.c1, out + 96);
+}
+static bool all_zero(const uint8_t* p, size_t n) {
+  for (size_t i = 0; i < n; ++i)
+    if (p[i]) return false;
+  return true;
+}
+static HFq fq_from_std_bytes(const uint8_t* p) {
+  U256 v = host::u256_from_le(p);
+  if (host::u256_geq(v, host::FQ_DESC.mod)) throw ZkpError(ZKP_ERR_INVALID_ARG, "partial: coordinate out of range");
+  return HFq::from_std(v);
+}
+static Jac<HFq> g1_from_bytes(const uint8_t* p) {
+  if (all_zero(p, 64)) return Jac<HFq>::inf();
+  return host::jac_from_aff(Affine<HFq>{fq_from_std_bytes(p), fq_from_std_bytes(p + 32), false});
+}
+static Jac<HFq2> g2_from_bytes(const uint8_t* p) {
+  if (all_zero(p, 128)) return Jac<HFq2>::inf();
+  return host::jac_from_aff(Affine<HFq2>{HFq2{fq_from_std_bytes(p), fq_from_std_bytes(p + 32)},
+                                         HFq2{fq_from_std_bytes(p + 64), fq_from_std_bytes(p + 96)}, false});
+}
+static void msm_out_to_partial(const DevicePipeline::MsmOut& m, int part, int nparts, zkp_partial* out) {
+  jac_to_bytes_g1(m.a, out->a);
+  jac_to_bytes_g1(m.b1, out->b1);
+  jac_to_bytes_g1(m.c, out->c);
+  jac_to_bytes_g1(m.h, out->h);
+  jac_to_bytes_g2(m.b2, out->b2);
+  out->part = (uint32_t)part;
+  out->nparts = (uint32_t)nparts;
+}
+
+void Prover::require_full() const {
+  if (nparts_ != 1)
+    throw ZkpError(ZKP_ERR_INVALID_ARG, "this prover holds one point range (part " + std::to_string(part_) + " of " +
+                                            std::to_string(nparts_) + "): use zkp_prove_partial + zkp_proof_combine");
+}
+
+void Prover::prove_partial(const uint8_t* wtns, size_t len, zkp_partial* out) {
+  WtnsView w = check_wtns(hdr_, wtns, len);
+  DevicePipeline::MsmOut m = devs_[0]->prove(w);
+  msm_out_to_partial(m, part_, nparts_, out);
+  std::lock_guard<std::mutex> lk(tmu_);
+  for (int i = 0; i < 5; ++i) last_ms_[i] = m.ms[i];
+  last_ms_[7] = m.ms[5];
+}
+
+void Prover::prove_partial_staged(int slot, zkp_partial* out) {
+  DevicePipeline::MsmOut m = devs_[0]->prove_staged(slot);
+  msm_out_to_partial(m, part_, nparts_, out);
+  std::lock_guard<std::mutex> lk(tmu_);
+  for (int i = 0; i < 5; ++i) last_ms_[i] = m.ms[i];
+  last_ms_[7] = m.ms[5];
+}
+
+void proof_combine(const uint8_t* zkey, size_t len, const zkp_partial* parts, int nparts, const uint8_t* wtns,
+                   size_t wlen, const uint8_t* r32, const uint8_t* s32, zkp_proof* out) {
+  if (nparts < 1) throw ZkpError(ZKP_ERR_INVALID_ARG, "no partials");
+  ZkeyParsed z = parse_zkey(zkey, len, false);
+  WtnsView w = check_wtns(z.hdr, wtns, wlen);
+  std::vector<int> seen(nparts, 0);
+  DevicePipeline::MsmOut m;
+  m.a = m.b1 = m.c = m.h = Jac<HFq>::inf();
+  m.b2 = Jac<HFq2>::inf();
+  for (int i = 0; i < nparts; ++i) {
+    const zkp_partial& p = parts[i];
+    if ((int)p.nparts != nparts || p.part >= p.nparts || seen[p.part]++)
+      throw ZkpError(ZKP_ERR_INVALID_ARG, "partials must be parts 0..nparts-1 of one split, each exactly once");
+    m.a = host::jac_add(m.a, g1_from_bytes(p.a));
+    m.b1 = host::jac_add(m.b1, g1_from_bytes(p.b1));
+    m.c = host::jac_add(m.c, g1_from_bytes(p.c));
+    m.h = host::jac_add(m.h, g1_from_bytes(p.h));
+    m.b2 = host::jac_add(m.b2, g2_from_bytes(p.b2));
+  }
+  assemble(z.hdr, m, w, r32, s32, out);
+}
+
 void Prover::prove(const uint8_t* wtns, size_t len, const uint8_t* r32, const uint8_t* s32, zkp_proof* out) {
+  require_full();
   auto t0 = std::chrono::steady_clock::now();
   WtnsView w = check_wtns(hdr_, wtns, len);
   DevicePipeline& d = *devs_[rr_.fetch_add(1) % devs_.size()];
@@ -655,6 +761,7 @@ void Prover::prove(const uint8_t* wtns, size_t len, const uint8_t* r32, const ui
 
 void Prover::prove_batch(const uint8_t* const* wtns, const size_t* lens, int n, const uint8_t* const* r32s,
                          const uint8_t* const* s32s, zkp_proof* outs) {
+  require_full();
   std::atomic<int> next{0};
   std::vector<std::exception_ptr> errs(devs_.size());
   std::vector<std::thread> th;
@@ -701,6 +808,7 @@ void Prover::stage(int dev, int slot, const uint8_t* wtns, size_t len) {
 }
 
 void Prover::prove_staged(int dev, int slot, const uint8_t* r32, const uint8_t* s32, zkp_proof* out) {
+  require_full();
   if (dev < 0 || dev >= (int)devs_.size()) throw ZkpError(ZKP_ERR_INVALID_ARG, "device index out of range");
   auto t0 = std::chrono::steady_clock::now();
   DevicePipeline::MsmOut m = devs_[dev]->prove_staged(slot);

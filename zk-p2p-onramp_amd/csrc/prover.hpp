@@ -62,7 +62,8 @@ class DevicePipeline;
 
 class Prover {
  public:
-  Prover(const uint8_t* zkey, size_t len, const std::vector<int>& devices);
+  // part / nparts > 1: hold only point slice `part` (one device) -> prove_partial only
+  Prover(const uint8_t* zkey, size_t len, const std::vector<int>& devices, int part = 0, int nparts = 1);
   ~Prover();
   const ZkeyHeader& header() const { return hdr_; }
   // r32/s32 nullable (CSPRNG).  Thread-safe.
@@ -78,12 +79,19 @@ class Prover {
   void set_instrument(bool on);
   void kernel_stats(double* out, int n) const;
   int device_count() const { return (int)devs_.size(); }
+  // point-range split of one proof: this slice's MSM partial sums
+  void prove_partial(const uint8_t* wtns, size_t len, zkp_partial* out);
+  void prove_partial_staged(int slot, zkp_partial* out);
+  int part() const { return part_; }
+  int nparts() const { return nparts_; }
   // MSM configuration of device 0: [0] witness c, [1] witness depth, [2] witness groups,
   // [3] H c, [4] H depth, [5] H groups, [6] base-table bytes per device
   void msm_config(double* out, int n) const;
 
  private:
+  void require_full() const;
   ZkeyHeader hdr_;
+  int part_ = 0, nparts_ = 1;
   std::vector<std::unique_ptr<DevicePipeline>> devs_;
   std::vector<std::vector<std::vector<uint8_t>>> staged_pub_;  // [dev][slot] -> first (nPub+1)*32 witness bytes
   mutable std::mutex smu_;
@@ -92,6 +100,11 @@ class Prover {
   float last_ms_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   friend class DevicePipeline;
 };
+
+// sum the partials of one split (host only: parses the zkey header, no device) and
+// assemble the proof exactly as Prover::prove would
+void proof_combine(const uint8_t* zkey, size_t len, const zkp_partial* parts, int nparts, const uint8_t* wtns,
+                   size_t wlen, const uint8_t* r32, const uint8_t* s32, zkp_proof* out);
 
 // kernel-level helpers (C-ABI zkp_msm_g1/g2, zkp_ntt_fr)
 // c / depth: window bits and base-table depth (0 = automatic, as the prover)

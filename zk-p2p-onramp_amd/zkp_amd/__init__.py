@@ -102,11 +102,17 @@ def load_library(path: str = LIB_PATH):
         lib.zkp_msm.argtypes = [ctypes.c_int, ctypes.c_int, u8p, u8p, sz, ctypes.c_int, ctypes.c_int, u8p,
                                 ctypes.POINTER(ctypes.c_int)]
         lib.zkp_prover_msm_config.argtypes = [P, ctypes.POINTER(ctypes.c_double), ctypes.c_int]
+        lib.zkp_prover_load_part.argtypes = [u8p, sz, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(P)]
+        lib.zkp_prove_partial.argtypes = [P, u8p, sz, ctypes.c_char_p]
+        lib.zkp_prove_partial_staged.argtypes = [P, ctypes.c_int, ctypes.c_char_p]
+        lib.zkp_proof_combine.argtypes = [u8p, sz, ctypes.c_char_p, ctypes.c_int, u8p, sz, u8p, u8p,
+                                          ctypes.POINTER(_Proof)]
         for name in ("zkp_prover_load_mem", "zkp_prover_load_file", "zkp_prover_info", "zkp_prove",
                      "zkp_prove_batch", "zkp_prove_files", "zkp_proof_json", "zkp_public_json",
                      "zkp_prover_timings", "zkp_msm_g1", "zkp_msm_g2", "zkp_ntt_fr", "zkp_quotient",
                      "zkp_witness_stage", "zkp_prove_staged", "zkp_prover_instrument", "zkp_prover_kernel_stats",
-                     "zkp_bench_msm", "zkp_bench_ntt", "zkp_msm", "zkp_prover_msm_config"):
+                     "zkp_bench_msm", "zkp_bench_ntt", "zkp_msm", "zkp_prover_msm_config",
+                     "zkp_prover_load_part", "zkp_prove_partial", "zkp_prove_partial_staged", "zkp_proof_combine"):
             getattr(lib, name).restype = ctypes.c_int
         _lib = lib
         return lib
@@ -117,10 +123,16 @@ def _check(st: int):
         raise ZkpError(st, load_library().zkp_last_error().decode())
 
 
-def _buf(data: bytes):
-    """(ctypes uint8 pointer, keepalive) for an immutable bytes-like object."""
-    arr = (ctypes.c_uint8 * len(data)).from_buffer_copy(data) if len(data) else (ctypes.c_uint8 * 1)()
-    return ctypes.cast(arr, ctypes.POINTER(ctypes.c_uint8)), arr
+def _buf(data):
+    """(ctypes uint8 pointer, keepalive) for a bytes-like object, without copying bytes /
+    bytearray (witnesses are hundreds of MB; the C side only reads)."""
+    if isinstance(data, bytes):
+        return ctypes.cast(ctypes.c_char_p(data), ctypes.POINTER(ctypes.c_uint8)), data
+    if isinstance(data, bytearray) and len(data):
+        arr = (ctypes.c_uint8 * len(data)).from_buffer(data)
+        return ctypes.cast(arr, ctypes.POINTER(ctypes.c_uint8)), arr
+    data = bytes(data)
+    return ctypes.cast(ctypes.c_char_p(data), ctypes.POINTER(ctypes.c_uint8)), data
 
 
 def _le(b) -> int:
@@ -134,13 +146,27 @@ def version() -> str:
 class Prover:
     """A zkey resident in HBM of one or more devices (loaded once, reused per proof)."""
 
-    def __init__(self, zkey, devices=None):
+    def __init__(self, zkey, devices=None, part=None, nparts=None):
+        """part / nparts: hold only point slice `part` of `nparts` on devices[0] (the
+        point-range split of one proof over several GPUs) -> prove_partial only."""
         lib = load_library()
         h = ctypes.c_void_p()
         devs = list(devices or [])
         darr = (ctypes.c_int * max(1, len(devs)))(*devs) if devs else None
         dptr = ctypes.cast(darr, ctypes.POINTER(ctypes.c_int)) if darr is not None else None
-        if hasattr(zkey, "ptr") and hasattr(zkey, "len"):  # library-owned buffer (e.g. synth.ZkeyBuffer)
+        self.part, self.nparts = (part or 0), (nparts or 1)
+        if nparts is not None:
+            if hasattr(zkey, "ptr") and hasattr(zkey, "len"):
+                _check(lib.zkp_prover_load_part(ctypes.cast(zkey.ptr, ctypes.POINTER(ctypes.c_uint8)), zkey.len,
+                                                devs[0] if devs else 0, self.part, self.nparts, ctypes.byref(h)))
+            else:
+                if not isinstance(zkey, (bytes, bytearray, memoryview)):
+                    zkey = open(zkey, "rb").read()
+                p, keep = _buf(bytes(zkey))
+                _check(lib.zkp_prover_load_part(p, len(zkey), devs[0] if devs else 0, self.part, self.nparts,
+                                                ctypes.byref(h)))
+                del keep
+        elif hasattr(zkey, "ptr") and hasattr(zkey, "len"):  # library-owned buffer (e.g. synth.ZkeyBuffer)
             _check(lib.zkp_prover_load_mem(ctypes.cast(zkey.ptr, ctypes.POINTER(ctypes.c_uint8)), zkey.len, dptr,
                                            len(devs), ctypes.byref(h)))
         elif isinstance(zkey, (bytes, bytearray, memoryview)):
@@ -256,6 +282,18 @@ class Prover:
     def instrument(self, on: bool = True):
         _check(load_library().zkp_prover_instrument(self._h, 1 if on else 0))
 
+    def prove_partial(self, wtns: bytes) -> bytes:
+        """This prover's slice of the five MSMs for one witness: a 392-byte zkp_partial."""
+        wp, wk = _buf(wtns)
+        out = ctypes.create_string_buffer(PARTIAL_BYTES)
+        _check(load_library().zkp_prove_partial(self._h, wp, len(wtns), out))
+        return out.raw
+
+    def prove_partial_staged(self, slot: int) -> bytes:
+        out = ctypes.create_string_buffer(PARTIAL_BYTES)
+        _check(load_library().zkp_prove_partial_staged(self._h, slot, out))
+        return out.raw
+
     def msm_config(self):
         out = (ctypes.c_double * 7)()
         _check(load_library().zkp_prover_msm_config(self._h, out, 7))
@@ -331,6 +369,48 @@ class _Groth16:
 
 
 groth16 = _Groth16()
+
+PARTIAL_BYTES = 392  # sizeof(zkp_partial)
+
+
+def proof_combine_raw(zkey, partials, wtns: bytes, r=None, s=None):
+    """Host-only: sum the partials (392-byte zkp_partial each, any order) of one split and
+    assemble the proof -> same tuple as Prover.prove_raw."""
+    lib = load_library()
+    blob = b"".join(bytes(p) for p in partials)
+    if len(blob) != PARTIAL_BYTES * len(partials):
+        raise ValueError("each partial must be %d bytes" % PARTIAL_BYTES)
+    if hasattr(zkey, "ptr") and hasattr(zkey, "len"):
+        zp, zlen, zk = ctypes.cast(zkey.ptr, ctypes.POINTER(ctypes.c_uint8)), zkey.len, None
+    else:
+        if not isinstance(zkey, (bytes, bytearray, memoryview)):
+            zkey = open(zkey, "rb").read()
+        zp, zk = _buf(bytes(zkey))
+        zlen = len(zkey)
+    wp, wk = _buf(wtns)
+    rp, rk = Prover._scalar(r)
+    sp, sk = Prover._scalar(s)
+    npub = 4096  # public-signal capacity (the Venmo circuit has 26)
+    pub = (ctypes.c_uint8 * (32 * npub))()
+    pr = _Proof()
+    pr.public_capacity = npub
+    pr.public_signals = ctypes.cast(pub, ctypes.POINTER(ctypes.c_uint8))
+    _check(lib.zkp_proof_combine(zp, zlen, blob, len(partials), wp, len(wtns), rp, sp, ctypes.byref(pr)))
+    if pr.n_public > npub:
+        raise ZkpError(1, "more than %d public signals" % npub)
+    return _unpack_proof(pr, pub)
+
+
+def partial_from_points(a, b1, c, h, b2, part: int, nparts: int) -> bytes:
+    """Encode affine partial sums (oracle tuples, None = infinity) as a zkp_partial."""
+    def g1(p):
+        return bytes(64) if p is None else int(p[0]).to_bytes(32, "little") + int(p[1]).to_bytes(32, "little")
+
+    def g2(p):
+        if p is None:
+            return bytes(128)
+        return b"".join(int(v).to_bytes(32, "little") for v in (p[0][0], p[0][1], p[1][0], p[1][1]))
+    return g1(a) + g1(b1) + g1(c) + g1(h) + g2(b2) + int(part).to_bytes(4, "little") + int(nparts).to_bytes(4, "little")
 
 
 def _msm(points_lem, scalars_le, g2, device, window_bits, table_depth):
