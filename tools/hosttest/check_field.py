@@ -24,6 +24,21 @@ def main(n=300):
         lines.append("canonq %s" % w8(a)); checks.append(("canonq", lambda v, a=a: v == a % P))
         x, y = rnd.randrange(2 * R), rnd.randrange(2 * R)
         lines.append("mulr %s %s" % (w8(x), w8(y))); checks.append(("mulr", lambda v, x=x, y=y: v % R == x * y * inv_rp_r % R and v < 2 * R))
+    # lazy subtractions feeding multiplications (field.hpp lsub / rsub), incl. extremes
+    edge = [0, 1, P - 1, P, P + 1, 2 * P - 1]
+    pairs = [(rnd.randrange(2 * P), rnd.randrange(2 * P)) for _ in range(n)] + [(a, b) for a in edge for b in edge]
+    for a, b in pairs:
+        c = rnd.randrange(2 * P)
+        lines.append("lsubmulq %s %s %s" % (w8(a), w8(b), w8(c)))
+        checks.append(("lsubmulq", lambda v, a=a, b=b, c=c: v % P == (a - b) * c * inv_rp_p % P and v < 2 * P))
+        lines.append("lsubsqrq %s %s" % (w8(a), w8(b)))
+        checks.append(("lsubsqrq", lambda v, a=a, b=b: v % P == (a - b) * (a - b) * inv_rp_p % P and v < 2 * P))
+        for cc in (c, 2 * P - 1):
+            lines.append("rsubmulq %s %s %s" % (w8(a), w8(b), w8(cc)))
+            checks.append(("rsubmulq", lambda v, a=a, b=b, c=cc: v % P == (a - b) * c * inv_rp_p % P and v < 2 * P))
+        x, y, wv = a % (2 * R), b % (2 * R), rnd.randrange(2 * R)
+        lines.append("rsubmulr %s %s %s" % (w8(x), w8(y), w8(wv)))
+        checks.append(("rsubmulr", lambda v, x=x, y=y, w=wv: v % R == (x - y) * w * inv_rp_r % R and v < 2 * R))
     for z in (0, P):
         lines.append("iszq %s" % w8(z)); checks.append(("iszq", lambda v: v == 1))
     out = subprocess.run([BIN], input="\n".join(lines) + "\n", capture_output=True, text=True).stdout.strip().split("\n")

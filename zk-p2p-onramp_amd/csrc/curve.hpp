@@ -98,40 +98,47 @@ ZDEV Xyzz<F> xyzz_dbl(const Xyzz<F>& p) {
   return r;
 }
 
-// acc += q (q affine, may be infinity)  — madd-2008-s
+// acc += (neg ? -q : q) (q affine, may be infinity)  — madd-2008-s.  The common path
+// uses lazy subtractions (P, R: lsub; Q - X3 and -y: rsub) where the value only feeds
+// a multiplication; zero tests run on PP = P^2 and RR = R^2, which are < 2m.
 template <class F>
-ZDEV void xyzz_add_aff(Xyzz<F>& acc, const Aff<F>& q) {
+ZDEV void xyzz_add_aff(Xyzz<F>& acc, const Aff<F>& q, bool neg = false) {
   if (aff_is_inf(q)) return;
   if (xyzz_is_inf(acc)) {
     acc.x = q.x;
-    acc.y = q.y;
+    acc.y = neg ? sub(f_zero<F>(), q.y) : q.y;
     acc.zz = f_one<F>();
     acc.zzz = f_one<F>();
     return;
   }
+  const F qy = neg ? rsub(f_zero<F>(), q.y) : q.y;  // mul operand only
   F U2 = mul(q.x, acc.zz);
-  F S2 = mul(q.y, acc.zzz);
-  F P = sub(U2, acc.x);
-  F R = sub(S2, acc.y);
-  if (is_zero(P)) {
-    if (is_zero(R))
-      acc = xyzz_dbl_aff(q);
-    else
+  F S2 = mul(qy, acc.zzz);
+  F P = lsub(U2, acc.x);
+  F R = lsub(S2, acc.y);
+  F PP = sqr(P);
+  F RR = sqr(R);
+  if (is_zero(PP)) {
+    if (is_zero(RR)) {
+      Aff<F> qs = q;
+      if (neg) qs.y = sub(f_zero<F>(), q.y);
+      acc = xyzz_dbl_aff(qs);
+    } else {
       acc = xyzz_inf<F>();
+    }
     return;
   }
-  F PP = sqr(P);
   F PPP = mul(P, PP);
   F Q = mul(acc.x, PP);
-  F X3 = sub(sub(sqr(R), PPP), dbl(Q));
-  F Y3 = sub(mul(R, sub(Q, X3)), mul(acc.y, PPP));
+  F X3 = sub(sub(RR, PPP), dbl(Q));
+  F Y3 = sub(mul(R, rsub(Q, X3)), mul(acc.y, PPP));
   acc.zz = mul(acc.zz, PP);
   acc.zzz = mul(acc.zzz, PPP);
   acc.x = X3;
   acc.y = Y3;
 }
 
-// acc += q (both XYZZ) — add-2008-s
+// acc += q (both XYZZ) — add-2008-s, with the same lazy subtractions as xyzz_add_aff
 template <class F>
 ZDEV void xyzz_add(Xyzz<F>& acc, const Xyzz<F>& q) {
   if (xyzz_is_inf(q)) return;
@@ -143,20 +150,21 @@ ZDEV void xyzz_add(Xyzz<F>& acc, const Xyzz<F>& q) {
   F U2 = mul(q.x, acc.zz);
   F S1 = mul(acc.y, q.zzz);
   F S2 = mul(q.y, acc.zzz);
-  F P = sub(U2, U1);
-  F R = sub(S2, S1);
-  if (is_zero(P)) {
-    if (is_zero(R))
+  F P = lsub(U2, U1);
+  F R = lsub(S2, S1);
+  F PP = sqr(P);
+  F RR = sqr(R);
+  if (is_zero(PP)) {
+    if (is_zero(RR))
       acc = xyzz_dbl(acc);
     else
       acc = xyzz_inf<F>();
     return;
   }
-  F PP = sqr(P);
   F PPP = mul(P, PP);
   F Q = mul(U1, PP);
-  F X3 = sub(sub(sqr(R), PPP), dbl(Q));
-  F Y3 = sub(mul(R, sub(Q, X3)), mul(S1, PPP));
+  F X3 = sub(sub(RR, PPP), dbl(Q));
+  F Y3 = sub(mul(R, rsub(Q, X3)), mul(S1, PPP));
   acc.zz = mul(mul(acc.zz, q.zz), PP);
   acc.zzz = mul(mul(acc.zzz, q.zzz), PPP);
   acc.x = X3;

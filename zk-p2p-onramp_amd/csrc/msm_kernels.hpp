@@ -116,9 +116,7 @@ ZDEV void accumulate(uint32_t t, const uint32_t* __restrict__ points, const uint
   Xyzz<F> acc = xyzz_inf<F>();
   for (uint32_t j = s0; j < s1; ++j) {
     const uint32_t v = vals[j];
-    Aff<F> p = load_aff<F>(points, v & 0x7fffffffu);
-    if (v >> 31) p.y = sub(f_zero<F>(), p.y);
-    xyzz_add_aff(acc, p);
+    xyzz_add_aff(acc, load_aff<F>(points, v & 0x7fffffffu), (v >> 31) != 0);
   }
   store_xyzz(out, t, acc);
 }

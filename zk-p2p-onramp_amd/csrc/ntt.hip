@@ -69,8 +69,8 @@ __global__ __launch_bounds__(TPB) void k_ntt_pass(uint32_t* __restrict__ data, i
         y.v[l] = lds[l * E + e1];
       }
       Fr s = add(x, y);
-      Fr d = sub(x, y);
-      if (i) d = mul(d, load_fe<FrCfg>(loc + (size_t)(i << (t + LOC_LOG - b)) * 8));
+      // x - y only feeds the twiddle multiply when i != 0: raw (unnormalised) subtraction
+      Fr d = i ? mul(rsub(x, y), load_fe<FrCfg>(loc + (size_t)(i << (t + LOC_LOG - b)) * 8)) : sub(x, y);
 #pragma unroll
       for (int l = 0; l < NL; ++l) {
         lds[l * E + e0] = s.v[l];
