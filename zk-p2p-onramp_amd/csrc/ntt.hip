@@ -12,9 +12,10 @@ namespace zkp {
 namespace {
 
 constexpr int TPB = 256;
-constexpr int LOG_TILE = 10;  // elements per workgroup tile (n1 * C = 1024, 36 KiB of LDS)
+constexpr int LOG_TILE = 10;  // elements per workgroup tile (1024, 36 KiB of LDS)
 constexpr int LOC_LOG = 10;   // local-root table: w_1024^e, e < 512
 constexpr int MAX_PASS_BITS = 8;
+constexpr int MAX_TW = 1 << (MAX_PASS_BITS - 1);  // stage roots of a 2^b-point DFT, b <= 8
 
 __device__ __forceinline__ uint32_t brev(uint32_t x, int b) { return __builtin_bitreverse32(x) >> (32 - b); }
 
@@ -26,51 +27,53 @@ __device__ __forceinline__ Fr tw_pow(const uint32_t* __restrict__ lo, const uint
   return mul(a, b);
 }
 
-// One pass over blocks of size 2^lm: n1 = 2^b point DFTs over the strided index,
-// tile = 2^lc consecutive columns.  dit: twiddle before the DFT, else after.
-__global__ __launch_bounds__(TPB) void k_ntt_pass(uint32_t* __restrict__ data, int k, int lm, int b, int lc, int dit,
-                                                  const uint32_t* __restrict__ loc,
-                                                  const uint32_t* __restrict__ tw_lo,
-                                                  const uint32_t* __restrict__ tw_hi, int h) {
-  __shared__ uint32_t lds[NL << LOG_TILE];  // SoA: lds[limb * E + element]
-  const int E = 1 << (b + lc);
-  const int C = 1 << lc;
-  const uint32_t n2 = 1u << (lm - b);
-  const uint32_t tiles_per_block = n2 >> lc;
-  const uint32_t tile = blockIdx.x;
-  const uint32_t blk = tile / tiles_per_block;
-  const uint32_t col0 = (tile - blk * tiles_per_block) << lc;
-  const size_t base = (size_t)blk << lm;
-  const int tw_shift = k - lm;  // w_m^e = w_n^(e << (k - lm))
+// Tile geometry of one pass over blocks of 2^lm elements (2^b rows x n2 = 2^(lm-b)
+// columns): a tile holds 2^lbt whole blocks (innermost passes, n2 small) or one block's
+// 2^b rows x 2^lc consecutive columns; E = 2^(lbt + b + lc) elements.
+struct Tile {
+  int lm, b, lc, lbt;
+};
 
-  for (int e = threadIdx.x; e < E; e += TPB) {
-    const uint32_t row = (uint32_t)e >> lc, col = (uint32_t)e & (C - 1);
-    const size_t g = base + (size_t)row * n2 + col0 + col;
-    Fr x = load_fe<FrCfg>(data + g * 8);
-    if (dit) {
-      const uint32_t ex = (col0 + col) * row;
-      if (ex) x = mul(x, tw_pow(tw_lo, tw_hi, ex << tw_shift, h));
-    }
+// the per-stage roots w_(2^b)^j, j < 2^(b-1), staged in LDS (9-limb SoA)
+__device__ __forceinline__ void stage_roots(uint32_t* __restrict__ ltw, const uint32_t* __restrict__ loc, int b) {
+  const int TW = 1 << (b - 1);
+  for (int j = threadIdx.x; j < TW; j += TPB) {
+    const Fr x = load_fe<FrCfg>(loc + (size_t)(j << (LOC_LOG - b)) * 8);
 #pragma unroll
-    for (int l = 0; l < NL; ++l) lds[l * E + e] = x.v[l];
+    for (int l = 0; l < NL; ++l) ltw[l * MAX_TW + j] = x.v[l];
   }
-  __syncthreads();
+}
+
+// b radix-2 DIF stages on the LDS tile (rows natural in, bit-reversed out)
+__device__ __forceinline__ void dft_stages(uint32_t* __restrict__ lds, const uint32_t* __restrict__ ltw, int E, int b,
+                                           int lc) {
+  const uint32_t C = 1u << lc;
   for (int t = 0; t < b; ++t) {
     const int lhalf = b - 1 - t;
     for (int q = threadIdx.x; q < (E >> 1); q += TPB) {
-      const uint32_t col = (uint32_t)q & (C - 1), bq = (uint32_t)q >> lc;
+      const uint32_t col = (uint32_t)q & (C - 1), bq = ((uint32_t)q >> lc) & ((1u << (b - 1)) - 1);
+      const uint32_t bl = (uint32_t)q >> (lc + b - 1);
       const uint32_t grp = bq >> lhalf, i = bq & ((1u << lhalf) - 1);
       const uint32_t r0 = (grp << (lhalf + 1)) + i, r1 = r0 + (1u << lhalf);
-      const int e0 = (int)((r0 << lc) + col), e1 = (int)((r1 << lc) + col);
+      const int base = (int)(bl << (b + lc));
+      const int e0 = base + (int)((r0 << lc) + col), e1 = base + (int)((r1 << lc) + col);
       Fr x, y;
 #pragma unroll
       for (int l = 0; l < NL; ++l) {
         x.v[l] = lds[l * E + e0];
         y.v[l] = lds[l * E + e1];
       }
-      Fr s = add(x, y);
-      // x - y only feeds the twiddle multiply when i != 0: raw (unnormalised) subtraction
-      Fr d = i ? mul(rsub(x, y), load_fe<FrCfg>(loc + (size_t)(i << (t + LOC_LOG - b)) * 8)) : sub(x, y);
+      const Fr s = add(x, y);
+      Fr d;
+      if (i) {
+        Fr w;
+        const uint32_t j = i << t;  // w_(2^(lhalf+1))^i = w_(2^b)^(i 2^t)
+#pragma unroll
+        for (int l = 0; l < NL; ++l) w.v[l] = ltw[l * MAX_TW + j];
+        d = mul(rsub(x, y), w);  // x - y only feeds the multiply: raw subtraction
+      } else {
+        d = sub(x, y);
+      }
 #pragma unroll
       for (int l = 0; l < NL; ++l) {
         lds[l * E + e0] = s.v[l];
@@ -79,19 +82,107 @@ __global__ __launch_bounds__(TPB) void k_ntt_pass(uint32_t* __restrict__ data, i
     }
     __syncthreads();
   }
+}
+
+// element e of tile `tile` -> global index g and position in its block
+__device__ __forceinline__ void tile_coords(const Tile& T, uint32_t tile, int e, size_t& g, uint32_t& pos) {
+  const uint32_t C = 1u << T.lc, n2 = 1u << (T.lm - T.b);
+  const uint32_t col = (uint32_t)e & (C - 1);
+  const uint32_t row = ((uint32_t)e >> T.lc) & ((1u << T.b) - 1);
+  const uint32_t bl = (uint32_t)e >> (T.lc + T.b);
+  size_t block;
+  uint32_t col0;
+  if (T.lbt > 0) {
+    block = ((size_t)tile << T.lbt) + bl;
+    col0 = 0;
+  } else {
+    const uint32_t tpb = n2 >> T.lc;
+    block = tile / tpb;
+    col0 = (tile - (uint32_t)block * tpb) << T.lc;
+  }
+  pos = row * n2 + col0 + col;
+  g = (block << T.lm) + pos;
+}
+
+// LDS index holding output row k1 of element e's (block, column) after dft_stages
+__device__ __forceinline__ int brev_src(const Tile& T, int e) {
+  const int mask = ((1 << T.b) - 1) << T.lc;
+  const uint32_t k1 = ((uint32_t)e >> T.lc) & ((1u << T.b) - 1);
+  return (e & ~mask) | (int)(brev(k1, T.b) << T.lc);
+}
+
+// MODE 0: DIF pass (DFT, then inter-pass twiddle), 1: DIT pass (twiddle, then DFT),
+// 2: the fused innermost pair of coset_extend (lm == b): inverse-root DFT, coset key
+//    (table by digit-reversed position), forward-root DFT on one LDS-resident tile.
+// tw: w_(2^lm)^(col*row) by position in block (null when n2 == 1).
+template <int MODE>
+__global__ __launch_bounds__(TPB) void k_ntt(uint32_t* __restrict__ data, Tile T, const uint32_t* __restrict__ tw,
+                                             const uint32_t* __restrict__ locA, const uint32_t* __restrict__ locB,
+                                             const uint32_t* __restrict__ coset) {
+  __shared__ uint32_t lds[NL << LOG_TILE];  // SoA: lds[limb * E + element]
+  __shared__ uint32_t ltw[(MODE == 2 ? 2 : 1) * NL * MAX_TW];
+  const int E = 1 << (T.b + T.lc + T.lbt);
+  const uint32_t tile = blockIdx.x;
+  stage_roots(ltw, locA, T.b);
+  if (MODE == 2) stage_roots(ltw + NL * MAX_TW, locB, T.b);
   for (int e = threadIdx.x; e < E; e += TPB) {
-    const uint32_t k1 = (uint32_t)e >> lc, col = (uint32_t)e & (C - 1);
-    const int src = (int)((brev(k1, b) << lc) + col);
+    size_t g;
+    uint32_t pos;
+    tile_coords(T, tile, e, g, pos);
+    Fr x = load_fe<FrCfg>(data + g * 8);
+    if (MODE == 1 && tw) x = mul(x, load_fe<FrCfg>(tw + (size_t)pos * 8));
+#pragma unroll
+    for (int l = 0; l < NL; ++l) lds[l * E + e] = x.v[l];
+  }
+  __syncthreads();
+  dft_stages(lds, ltw, E, T.b, T.lc);
+  if (MODE == 2) {
+    // output row k1 (natural position in the block) sits at LDS row brev(k1): key it with
+    // g^f(pos)/n and put it back at row k1 as the forward DFT's input
+    Fr v[(1 << LOG_TILE) / TPB];
+    int idx = 0;
+    for (int e = threadIdx.x; e < E; e += TPB, ++idx) {
+      const int src = brev_src(T, e);
+      Fr x;
+#pragma unroll
+      for (int l = 0; l < NL; ++l) x.v[l] = lds[l * E + src];
+      size_t g;
+      uint32_t pos;
+      tile_coords(T, tile, e, g, pos);
+      v[idx] = mul(x, load_fe<FrCfg>(coset + g * 8));
+    }
+    __syncthreads();
+    idx = 0;
+    for (int e = threadIdx.x; e < E; e += TPB, ++idx) {
+#pragma unroll
+      for (int l = 0; l < NL; ++l) lds[l * E + e] = v[idx].v[l];
+    }
+    __syncthreads();
+    dft_stages(lds, ltw + NL * MAX_TW, E, T.b, T.lc);
+  }
+  for (int e = threadIdx.x; e < E; e += TPB) {
+    const int src = brev_src(T, e);
     Fr x;
 #pragma unroll
     for (int l = 0; l < NL; ++l) x.v[l] = lds[l * E + src];
-    if (!dit) {
-      const uint32_t ex = (col0 + col) * k1;
-      if (ex) x = mul(x, tw_pow(tw_lo, tw_hi, ex << tw_shift, h));
-    }
-    const size_t g = base + (size_t)k1 * n2 + col0 + col;
+    size_t g;
+    uint32_t pos;
+    tile_coords(T, tile, e, g, pos);
+    if (MODE == 0 && tw) x = mul(x, load_fe<FrCfg>(tw + (size_t)pos * 8));
     store_fe(data + g * 8, x);
   }
+}
+
+// tw[pos] = w_(2^lm)^(col * row), pos = row * n2 + col, from the two-level w_n tables
+__global__ __launch_bounds__(TPB) void k_pass_table(uint32_t* __restrict__ out, int k, int lm, int b,
+                                                    const uint32_t* __restrict__ lo, const uint32_t* __restrict__ hi,
+                                                    int h) {
+  const size_t pos = (size_t)blockIdx.x * TPB + threadIdx.x;
+  if (pos >= (size_t(1) << lm)) return;
+  const uint32_t n2 = 1u << (lm - b);
+  const uint32_t row = (uint32_t)(pos >> (lm - b)), col = (uint32_t)pos & (n2 - 1);
+  const uint32_t ex = (uint32_t)(((uint64_t)row * col) << (k - lm)) & (uint32_t)((uint64_t(1) << k) - 1);
+  store_fe(out + pos * 8, tw_pow(lo, hi, ex, h));
 }
 
 struct PassBits {
@@ -113,20 +204,20 @@ __device__ __forceinline__ uint32_t freq_of(uint32_t pos, int k, const PassBits&
   return f;
 }
 
-// mode 0: x * g^f(pos) / n ; mode 1: x / n
-__global__ __launch_bounds__(TPB) void k_scale(uint32_t* __restrict__ data, int k, PassBits pb, int mode,
-                                               const uint32_t* __restrict__ c_lo, const uint32_t* __restrict__ c_hi,
-                                               int h, const uint32_t* __restrict__ ninv) {
+// coset key table: out[pos] = g^f(pos) / n
+__global__ __launch_bounds__(TPB) void k_coset_table(uint32_t* __restrict__ out, int k, PassBits pb,
+                                                     const uint32_t* __restrict__ c_lo,
+                                                     const uint32_t* __restrict__ c_hi, int h) {
   const uint32_t pos = blockIdx.x * TPB + threadIdx.x;
   if (pos >= (1u << k)) return;
-  Fr x = load_fe<FrCfg>(data + (size_t)pos * 8);
-  if (mode == 0) {
-    const uint32_t f = freq_of(pos, k, pb);
-    x = mul(x, tw_pow(c_lo, c_hi, f, h));
-  } else {
-    x = mul(x, load_fe<FrCfg>(ninv));
-  }
-  store_fe(data + (size_t)pos * 8, x);
+  store_fe(out + (size_t)pos * 8, tw_pow(c_lo, c_hi, freq_of(pos, k, pb), h));
+}
+
+// x / n (inverse transform of the tests)
+__global__ __launch_bounds__(TPB) void k_scale(uint32_t* __restrict__ data, int k, const uint32_t* __restrict__ ninv) {
+  const uint32_t pos = blockIdx.x * TPB + threadIdx.x;
+  if (pos >= (1u << k)) return;
+  store_fe(data + (size_t)pos * 8, mul(load_fe<FrCfg>(data + (size_t)pos * 8), load_fe<FrCfg>(ninv)));
 }
 
 __global__ __launch_bounds__(TPB) void k_digit_reverse(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
@@ -191,6 +282,23 @@ HFr root_of_unity(int lg) {  // Fr.w[lg]
   return HFr::from_std(words8_to_u256(FR_ROOTS_W[lg]));
 }
 
+PassBits make_pb(const std::vector<int>& bits) {
+  PassBits pb{};
+  pb.n = (int)bits.size();
+  for (int i = 0; i < pb.n; ++i) pb.b[i] = bits[i];
+  return pb;
+}
+
+Tile make_tile(int k, int lm, int b) {
+  Tile T;
+  T.lm = lm;
+  T.b = b;
+  const int le = std::min(LOG_TILE, k);      // tile elements (log)
+  T.lc = std::min(le - b, lm - b);           // columns of one block in the tile
+  T.lbt = le - b - T.lc;                     // whole blocks per tile (innermost passes)
+  return T;
+}
+
 }  // namespace
 
 NttEngine::NttEngine(int log_n, hipStream_t stream) : log_n_(log_n), stream_(stream) {
@@ -202,6 +310,7 @@ NttEngine::NttEngine(int log_n, hipStream_t stream) : log_n_(log_n), stream_(str
     for (int i = 0; i < p; ++i) {
       const int b = (rem + (p - i) - 1) / (p - i);
       bits_.push_back(b);
+      lms_.push_back(rem);
       rem -= b;
     }
   }
@@ -224,55 +333,70 @@ NttEngine::NttEngine(int log_n, hipStream_t stream) : log_n_(log_n), stream_(str
   coset_lo_ = upload_powers(g, nlo, 1, ninv, stream_);
   coset_hi_ = upload_powers(g, nhi, nlo, one, stream_);
   ninv_ = upload_powers(one, 1, 1, ninv, stream_);
+  // per-pass twiddle tables (one multiply per element instead of lo*hi per element) and
+  // the coset key by digit-reversed position: ~3 n x 32 B of HBM
+  for (int dir = 0; dir < 2; ++dir) {
+    tw_pass_[dir].assign(bits_.size(), nullptr);
+    for (size_t p = 0; p < bits_.size(); ++p) {
+      const int lm = lms_[p], b = bits_[p];
+      if (lm == b) continue;  // innermost pass: n2 = 1, no twiddle
+      const size_t cnt = size_t(1) << lm;
+      HIPX(hipMalloc(&tw_pass_[dir][p], cnt * 32));
+      table_bytes_ += cnt * 32;
+      hipLaunchKernelGGL(k_pass_table, dim3((unsigned)((cnt + TPB - 1) / TPB)), dim3(TPB), 0, stream_,
+                         tw_pass_[dir][p], k, lm, b, tw_lo_[dir], tw_hi_[dir], h_);
+    }
+  }
+  if (k > 0) {
+    const size_t n = size_t(1) << k;
+    HIPX(hipMalloc(&coset_pos_, n * 32));
+    table_bytes_ += n * 32;
+    hipLaunchKernelGGL(k_coset_table, dim3((unsigned)((n + TPB - 1) / TPB)), dim3(TPB), 0, stream_, coset_pos_, k,
+                       make_pb(bits_), coset_lo_, coset_hi_, h_);
+  }
+  HIPX(hipGetLastError());
+  HIPX(hipStreamSynchronize(stream_));
 }
 
 NttEngine::~NttEngine() {
   for (uint32_t* p : {tw_lo_[0], tw_lo_[1], tw_hi_[0], tw_hi_[1], loc_[0], loc_[1], coset_lo_, coset_hi_, ninv_,
-                      scratch_})
+                      scratch_, coset_pos_})
     if (p) (void)hipFree(p);
+  for (auto& v : tw_pass_)
+    for (uint32_t* p : v)
+      if (p) (void)hipFree(p);
 }
 
-void NttEngine::dif_passes(uint32_t* data, bool inv) {
+// mode 0: DIF pass p, 1: DIT (transposed) pass p, 2: fused innermost pass (inverse then forward)
+void NttEngine::launch_pass(uint32_t* data, int mode, int p, bool inv) {
   const int k = log_n_;
-  int lm = k;
-  for (int b : bits_) {
-    const int lc = std::min(LOG_TILE - b, lm - b);
-    const size_t tiles = (size_t(1) << k) >> (b + lc);
-    hipLaunchKernelGGL(k_ntt_pass, dim3((unsigned)tiles), dim3(TPB), 0, stream_, data, k, lm, b, lc, 0,
-                       loc_[inv ? 1 : 0], tw_lo_[inv ? 1 : 0], tw_hi_[inv ? 1 : 0], h_);
-    lm -= b;
-  }
+  const Tile T = make_tile(k, lms_[p], bits_[p]);
+  const size_t tiles = (size_t(1) << k) >> (T.b + T.lc + T.lbt);
+  const int d = inv ? 1 : 0;
+  if (mode == 0)
+    hipLaunchKernelGGL(k_ntt<0>, dim3((unsigned)tiles), dim3(TPB), 0, stream_, data, T, tw_pass_[d][p], loc_[d],
+                       (const uint32_t*)nullptr, (const uint32_t*)nullptr);
+  else if (mode == 1)
+    hipLaunchKernelGGL(k_ntt<1>, dim3((unsigned)tiles), dim3(TPB), 0, stream_, data, T, tw_pass_[d][p], loc_[d],
+                       (const uint32_t*)nullptr, (const uint32_t*)nullptr);
+  else
+    hipLaunchKernelGGL(k_ntt<2>, dim3((unsigned)tiles), dim3(TPB), 0, stream_, data, T, (const uint32_t*)nullptr,
+                       loc_[1], loc_[0], coset_pos_);
 }
 
-void NttEngine::dit_passes(uint32_t* data, bool inv) {
-  const int k = log_n_;
+void NttEngine::dif_passes(uint32_t* data, bool inv, int first, int last) {
+  for (int p = first; p < last; ++p) launch_pass(data, 0, p, inv);
+}
+
+void NttEngine::dit_passes(uint32_t* data, bool inv, int first, int last) {
   // transposed passes in reverse order: block sizes grow back from the innermost
-  std::vector<int> lms;
-  int lm = k;
-  for (int b : bits_) {
-    lms.push_back(lm);
-    lm -= b;
-  }
-  for (int i = (int)bits_.size() - 1; i >= 0; --i) {
-    const int b = bits_[i], lmi = lms[i];
-    const int lc = std::min(LOG_TILE - b, lmi - b);
-    const size_t tiles = (size_t(1) << k) >> (b + lc);
-    hipLaunchKernelGGL(k_ntt_pass, dim3((unsigned)tiles), dim3(TPB), 0, stream_, data, k, lmi, b, lc, 1,
-                       loc_[inv ? 1 : 0], tw_lo_[inv ? 1 : 0], tw_hi_[inv ? 1 : 0], h_);
-  }
-}
-
-static PassBits make_pb(const std::vector<int>& bits) {
-  PassBits pb{};
-  pb.n = (int)bits.size();
-  for (int i = 0; i < pb.n; ++i) pb.b[i] = bits[i];
-  return pb;
+  for (int p = last - 1; p >= first; --p) launch_pass(data, 1, p, inv);
 }
 
 void NttEngine::scale(uint32_t* data, int mode) {
+  (void)mode;
   const size_t n = size_t(1) << log_n_;
-  hipLaunchKernelGGL(k_scale, dim3((unsigned)((n + TPB - 1) / TPB)), dim3(TPB), 0, stream_, data, log_n_,
-                     make_pb(bits_), mode, coset_lo_, coset_hi_, h_, ninv_);
+  hipLaunchKernelGGL(k_scale, dim3((unsigned)((n + TPB - 1) / TPB)), dim3(TPB), 0, stream_, data, log_n_, ninv_);
 }
 
 void NttEngine::digit_reverse(uint32_t* data, bool to_natural) {
@@ -288,22 +412,23 @@ void NttEngine::coset_extend(uint32_t* data) {
     // n = 1: coefficient = value; evaluation at g is the same constant
     return;
   }
-  dif_passes(data, true);
-  scale(data, 0);
-  dit_passes(data, false);
+  const int P = (int)bits_.size();
+  dif_passes(data, true, 0, P - 1);  // inverse, outer passes
+  launch_pass(data, 2, P - 1, true);  // innermost inverse pass + coset key + innermost forward pass
+  dit_passes(data, false, 0, P - 1);  // forward, outer passes (transposed, reverse order)
   HIPX(hipGetLastError());
 }
 
 void NttEngine::forward(uint32_t* data) {
   if (log_n_ == 0) return;
-  dif_passes(data, false);
+  dif_passes(data, false, 0, (int)bits_.size());
   digit_reverse(data, true);
   HIPX(hipGetLastError());
 }
 
 void NttEngine::inverse(uint32_t* data) {
   if (log_n_ == 0) return;
-  dif_passes(data, true);
+  dif_passes(data, true, 0, (int)bits_.size());
   scale(data, 1);
   digit_reverse(data, true);
   HIPX(hipGetLastError());

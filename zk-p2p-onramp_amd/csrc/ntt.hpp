@@ -6,13 +6,18 @@
 //   --x g^i-->  --NTT-->  evaluations on the coset g<w> (natural order)
 // with w = Fr.w[log2 n] and g = Fr.w[log2 n + 1] (ffjavascript convention).
 //
-// Multi-pass "four-step" structure: a pass splits the current block of size m
-// into n1 x n2, runs n1-point DFTs in LDS over the strided j1 index for a tile
-// of consecutive columns (radix-2 stages, LDS-resident), and multiplies by the
-// inter-pass twiddle w_m^(j2*k1).  The inverse runs these passes DIF-style
-// (natural in -> digit-reversed out); the forward runs the TRANSPOSED passes in
-// reverse order (digit-reversed in -> natural out), so no permutation pass is
-// ever needed; the coset key g^i / n is applied in digit-reversed index space.
+// Multi-pass "four-step" structure: a pass splits the current block of size m = 2^lm
+// into 2^b rows x n2 columns, runs 2^b-point DFTs in LDS over the strided row index
+// for a tile of consecutive columns (radix-2 stages on LDS-resident 9-limb values,
+// the stage roots staged in LDS), and multiplies by the inter-pass twiddle
+// w_m^(col*row), read from a per-(block size, direction) table indexed by the
+// element's position in the block (coalesced like the data; one multiply, no
+// exponent arithmetic).  The inverse runs these passes DIF-style (natural in ->
+// digit-reversed out); the forward runs the TRANSPOSED passes in reverse order
+// (digit-reversed in -> natural out), so no permutation pass is ever needed.  In
+// coset_extend the innermost inverse pass, the coset key g^f(pos)/n (a table in
+// digit-reversed position order) and the innermost forward pass are ONE kernel: the
+// tile never leaves LDS between them.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cstdint>
@@ -35,24 +40,32 @@ class NttEngine {
   void forward(uint32_t* data);  // A_j = sum a_i w^(ij)
   void inverse(uint32_t* data);  // a_i = n^-1 sum A_j w^(-ij)
   hipStream_t stream() const { return stream_; }
+  size_t table_bytes() const { return table_bytes_; }
 
  private:
-  void dif_passes(uint32_t* data, bool inverse_root);
-  void dit_passes(uint32_t* data, bool inverse_root);
+  // passes [first, last) of the DIF sequence (dir 1 = inverse root), resp. of the
+  // transposed DIT sequence in reverse order
+  void dif_passes(uint32_t* data, bool inv, int first, int last);
+  void dit_passes(uint32_t* data, bool inv, int first, int last);
+  void launch_pass(uint32_t* data, int mode, int p, bool inv);
   void scale(uint32_t* data, int mode);  // 0: x g^f(pos)/n   1: x 1/n (digit-reversed layout ok)
   void digit_reverse(uint32_t* data, bool to_natural);
   int log_n_;
   hipStream_t stream_;
   std::vector<int> bits_;  // pass radix bits (DIF order)
+  std::vector<int> lms_;   // block size log of each DIF pass
   int h_ = 0;              // split of the twiddle exponent tables
   // device tables (dev layout): [0] forward root, [1] inverse root
   uint32_t* tw_lo_[2] = {nullptr, nullptr};
   uint32_t* tw_hi_[2] = {nullptr, nullptr};
-  uint32_t* loc_[2] = {nullptr, nullptr};  // local roots w_(2^b)^e, for every b <= 10, e < 2^(b-1): packed by b
+  std::vector<uint32_t*> tw_pass_[2];      // per DIF pass p: w_(2^lm)^(col*row) by position in block (null: none)
+  uint32_t* loc_[2] = {nullptr, nullptr};  // local roots w_1024^e, e < 512
   uint32_t* coset_lo_ = nullptr;           // g^e / n, e < 2^h
   uint32_t* coset_hi_ = nullptr;           // g^(e 2^h)
+  uint32_t* coset_pos_ = nullptr;          // g^f(pos) / n by digit-reversed position
   uint32_t* ninv_ = nullptr;               // 1/n (dev form)
   uint32_t* scratch_ = nullptr;            // for digit_reverse (tests only)
+  size_t table_bytes_ = 0;
 };
 
 }  // namespace zkp

@@ -476,7 +476,6 @@ class DevicePipeline {
 
   // the whole device pipeline on a resident witness (caller holds mu_, ev_[0..1] recorded)
   MsmOut prove_dev(const uint32_t* d_wit) {
-    const ZkeyHeader& h = hdr_;
     // group-sum layout in dwin_: A | B1 | C (engine g1a) | H (g1h) | B2 (g2)
     uint32_t* wa = dwin_;
     uint32_t* wh = dwin_ + 3 * wina_;
