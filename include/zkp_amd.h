@@ -111,6 +111,11 @@ zkp_status zkp_prove_files(zkp_prover* p, const char* wtns_path, const char* pro
 zkp_status zkp_proof_json(const zkp_proof* proof, char* buf, size_t cap, size_t* needed);
 zkp_status zkp_public_json(const zkp_proof* proof, char* buf, size_t cap, size_t* needed);
 
+/* `snarkjs zkey export soliditycalldata` text of a proof + its public signals
+ * (reference circuit/scripts/generate_calldata.sh:3): a, b (G2 pairs in EIP-197
+ * [c1, c0] order, as Verifier.sol:184-188 expects), c, inputs as "0x" + 64 hex digits. */
+zkp_status zkp_proof_calldata(const zkp_proof* proof, char* buf, size_t cap, size_t* needed);
+
 /* Per-stage device timings (ms) of the last zkp_prove on this handle:
  * [0] wtns H2D, [1] buildABC, [2] NTT/quotient, [3] MSM G1 A,B1,C (own stream, overlaps
  * [1]-[2]), [4] MSM G2 B2 (own stream), [5] host assembly, [6] total wall, [7] MSM G1 H.

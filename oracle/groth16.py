@@ -161,6 +161,21 @@ def proof_from_json_obj(o) -> dict:
     return {"A": A, "B": B, "C": C}
 
 
+def verify_calldata(z: ZKey, calldata: str) -> bool:
+    """On-chain acceptance of `zkey export soliditycalldata` text: restates
+    Verifier.sol:359-375 verifyProof(a, b, c, input) -> verify(:340-358).  b arrives in the
+    EIP-197 [c1, c0] order (Pairing.G2Point stores X as [c1, c0], Verifier.sol:184-188)."""
+    a, b, c, inputs = json.loads("[" + calldata + "]")
+    h = lambda x: int(x, 16)
+    A = (h(a[0]), h(a[1]))
+    B = ((h(b[0][1]), h(b[0][0])), (h(b[1][1]), h(b[1][0])))
+    C = (h(c[0]), h(c[1]))
+    try:
+        return verify_with_zkey(z, [h(x) for x in inputs], {"A": A, "B": B, "C": C})
+    except ValueError:  # require() failures revert
+        return False
+
+
 def solidity_calldata(proof, public):
     """``zkey export soliditycalldata`` shape: G2 pairs reversed to [c1, c0]
     (reference SubmitOrderOnRampForm.tsx:36-46, Verifier.sol:366-369)."""

@@ -87,3 +87,11 @@ def test_errors(golden_dir):
     with pytest.raises(zkp_amd.ZkpError) as e:
         p.prove(binfile.write_binfile(b"wtns", 2, [(1, sec1), (2, sec2)]))
     assert e.value.status == 5
+
+
+def test_gpu_proof_calldata_accepted(golden_dir):
+    """GPU proof (random r, s) -> soliditycalldata -> restated Verifier.sol accepts it."""
+    zk, wt = _files(golden_dir, "venmo_mini")
+    z = binfile.read_zkey(zk)
+    proof, pub = zkp_amd.Prover(zk).prove_raw(wt)
+    assert groth16.verify_calldata(z, zkp_amd.solidity_calldata(proof, pub))

@@ -84,6 +84,31 @@ std::string public_json(const zkp_proof* p) {
   return s;
 }
 
+// "0x" + 64 hex digits of a 32-byte LE integer, quoted (snarkjs p256)
+std::string p256(const uint8_t* le32) {
+  static const char* hx = "0123456789abcdef";
+  std::string s = "\"0x";
+  for (int i = 31; i >= 0; --i) {
+    s += hx[le32[i] >> 4];
+    s += hx[le32[i] & 15];
+  }
+  return s + "\"";
+}
+
+// snarkjs 0.4.22 `zkey export soliditycalldata` (G2 pairs in EIP-197 [c1, c0] order)
+std::string calldata(const zkp_proof* p) {
+  std::string s = "[" + p256(p->pi_a[0]) + ", " + p256(p->pi_a[1]) + "],";
+  s += "[[" + p256(p->pi_b[0][1]) + ", " + p256(p->pi_b[0][0]) + "],[" + p256(p->pi_b[1][1]) + ", " +
+       p256(p->pi_b[1][0]) + "]],";
+  s += "[" + p256(p->pi_c[0]) + ", " + p256(p->pi_c[1]) + "],[";
+  const uint32_t n = std::min(p->n_public, p->public_capacity);
+  for (uint32_t i = 0; i < n && p->public_signals; ++i) {
+    if (i) s += ",";
+    s += p256(p->public_signals + 32 * i);
+  }
+  return s + "]";
+}
+
 zkp_status emit(const std::string& s, char* buf, size_t cap, size_t* needed) {
   if (needed) *needed = s.size() + 1;
   if (buf && cap >= s.size() + 1) {
@@ -210,6 +235,11 @@ zkp_status zkp_proof_json(const zkp_proof* proof, char* buf, size_t cap, size_t*
 zkp_status zkp_public_json(const zkp_proof* proof, char* buf, size_t cap, size_t* needed) {
   if (!proof) return fail(ZKP_ERR_INVALID_ARG, "null proof");
   return emit(public_json(proof), buf, cap, needed);
+}
+
+zkp_status zkp_proof_calldata(const zkp_proof* proof, char* buf, size_t cap, size_t* needed) {
+  if (!proof) return fail(ZKP_ERR_INVALID_ARG, "null proof");
+  return emit(calldata(proof), buf, cap, needed);
 }
 
 zkp_status zkp_prover_timings(const zkp_prover* p, float* ms, int n) {

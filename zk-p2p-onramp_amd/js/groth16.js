@@ -66,9 +66,46 @@ async function prove(zkeyFileName, witnessFileName, logger, opts) {
   return { proof, publicSignals: r.publicSignals };
 }
 
+// `snarkjs zkey export soliditycalldata` text (snarkjs 0.4.22 groth16ExportSolidityCallData,
+// called at reference circuit/scripts/generate_calldata.sh:3): 64-hex-digit "0x" words,
+// G2 coordinates in the EIP-197 [c1, c0] order that Verifier.sol:184-188 / :366-369 expects.
+function p256(n) {
+  let s = BigInt(n).toString(16);
+  while (s.length < 64) s = '0' + s;
+  return `"0x${s}"`;
+}
+
+async function exportSolidityCallData(proof, publicSignals) {
+  const inputs = publicSignals.map(p256).join(',');
+  return `[${p256(proof.pi_a[0])}, ${p256(proof.pi_a[1])}],` +
+    `[[${p256(proof.pi_b[0][1])}, ${p256(proof.pi_b[0][0])}],[${p256(proof.pi_b[1][1])}, ${p256(proof.pi_b[1][0])}]],` +
+    `[${p256(proof.pi_c[0])}, ${p256(proof.pi_c[1])}],` +
+    `[${inputs}]`;
+}
+
+// Argument list of Ramp.onRamp(uint256[2] _a, uint256[2][2] _b, uint256[2] _c, uint256[msgLen] _signals)
+// exactly as the app builds it (reference app/src/components/SubmitOrderOnRampForm.tsx:36-55:
+// pi_a / pi_c without the projective "1", each pi_b pair reversed to [c1, c0]).
+function onRampArgs(proof, publicSignals) {
+  return [
+    proof.pi_a.slice(0, 2),
+    proof.pi_b.slice(0, 2).map((g2point) => g2point.slice().reverse()),
+    proof.pi_c.slice(0, 2),
+    publicSignals,
+  ];
+}
+
 function release() {
   for (const h of provers.values()) addon.freeProver(h);
   provers.clear();
 }
 
-module.exports = { groth16: { prove }, prove, release, version: addon.version };
+module.exports = {
+  groth16: { prove },
+  zKey: { exportSolidityCallData },
+  prove,
+  exportSolidityCallData,
+  onRampArgs,
+  release,
+  version: addon.version,
+};

@@ -16,5 +16,11 @@ export declare const groth16: {
 };
 export declare function prove(zkey: Input, wtns: Input, logger?: Logger, opts?: ProveOptions):
   Promise<{ proof: Proof; publicSignals: string[] }>;
+export declare const zKey: {
+  exportSolidityCallData(proof: Proof, publicSignals: string[]): Promise<string>;
+};
+export declare function exportSolidityCallData(proof: Proof, publicSignals: string[]): Promise<string>;
+export declare function onRampArgs(proof: Proof, publicSignals: string[]):
+  [[string, string], [[string, string], [string, string]], [string, string], string[]];
 export declare function release(): void;
 export declare function version(): string;

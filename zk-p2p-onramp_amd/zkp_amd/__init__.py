@@ -102,6 +102,7 @@ def load_library(path: str = LIB_PATH):
         lib.zkp_msm.argtypes = [ctypes.c_int, ctypes.c_int, u8p, u8p, sz, ctypes.c_int, ctypes.c_int, u8p,
                                 ctypes.POINTER(ctypes.c_int)]
         lib.zkp_prover_msm_config.argtypes = [P, ctypes.POINTER(ctypes.c_double), ctypes.c_int]
+        lib.zkp_proof_calldata.argtypes = [ctypes.POINTER(_Proof), ctypes.c_char_p, sz, ctypes.POINTER(sz)]
         lib.zkp_prover_load_part.argtypes = [u8p, sz, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(P)]
         lib.zkp_prove_partial.argtypes = [P, u8p, sz, ctypes.c_char_p]
         lib.zkp_prove_partial_staged.argtypes = [P, ctypes.c_int, ctypes.c_char_p]
@@ -112,7 +113,7 @@ def load_library(path: str = LIB_PATH):
                      "zkp_prover_timings", "zkp_msm_g1", "zkp_msm_g2", "zkp_ntt_fr", "zkp_quotient",
                      "zkp_witness_stage", "zkp_prove_staged", "zkp_prover_instrument", "zkp_prover_kernel_stats",
                      "zkp_bench_msm", "zkp_bench_ntt", "zkp_msm", "zkp_prover_msm_config",
-                     "zkp_prover_load_part", "zkp_prove_partial", "zkp_prove_partial_staged", "zkp_proof_combine"):
+                     "zkp_prover_load_part", "zkp_prove_partial", "zkp_proof_calldata", "zkp_prove_partial_staged", "zkp_proof_combine"):
             getattr(lib, name).restype = ctypes.c_int
         _lib = lib
         return lib
@@ -399,6 +400,28 @@ def proof_combine_raw(zkey, partials, wtns: bytes, r=None, s=None):
     if pr.n_public > npub:
         raise ZkpError(1, "more than %d public signals" % npub)
     return _unpack_proof(pr, pub)
+
+
+def solidity_calldata(proof, public_signals) -> str:
+    """`snarkjs zkey export soliditycalldata` text via the C ABI (zkp_proof_calldata).
+    proof: ((ax, ay), ((bx0, bx1), (by0, by1)), (cx, cy)) as from Prover.prove_raw."""
+    (a, b, c) = proof
+    pr = _Proof()
+    for i in range(2):
+        pr.pi_a[i][:] = int(a[i]).to_bytes(32, "little")
+        pr.pi_c[i][:] = int(c[i]).to_bytes(32, "little")
+        for j in range(2):
+            pr.pi_b[i][j][:] = int(b[i][j]).to_bytes(32, "little")
+    pub = b"".join(int(x).to_bytes(32, "little") for x in public_signals) or bytes(32)
+    pbuf = (ctypes.c_uint8 * len(pub)).from_buffer_copy(pub)
+    pr.n_public = pr.public_capacity = len(public_signals)
+    pr.public_signals = ctypes.cast(pbuf, ctypes.POINTER(ctypes.c_uint8))
+    need = ctypes.c_size_t()
+    lib = load_library()
+    _check(lib.zkp_proof_calldata(ctypes.byref(pr), None, 0, ctypes.byref(need)))
+    out = ctypes.create_string_buffer(need.value)
+    _check(lib.zkp_proof_calldata(ctypes.byref(pr), out, need.value, ctypes.byref(need)))
+    return out.value.decode()
 
 
 def partial_from_points(a, b1, c, h, b2, part: int, nparts: int) -> bytes:
