@@ -72,6 +72,17 @@ typedef struct zkp_partial {
 zkp_status zkp_prover_load_file(const char* zkey_path, const int* devices, int ndev, zkp_prover** out);
 zkp_status zkp_prover_load_mem(const uint8_t* zkey, size_t len, const int* devices, int ndev, zkp_prover** out);
 
+/* Chunked / compressed proving keys (the app's circuit.zkey{b..k}.gz: reference
+ * app/src/helpers/zkp.ts:11-13,51-68).  zkp_prover_load_file and zkp_zkey_read accept a
+ * path that exists (gzip detected by magic), else path.gz, else the chunks
+ * path{a..z}[.gz] in suffix order.  Chunks are either a byte split of one binfile or
+ * per-chunk "zkey" binfiles holding disjoint sections (told apart by content). */
+zkp_status zkp_prover_load_chunks(const char* const* paths, int n, const int* devices, int ndev, zkp_prover** out);
+/* Host only: the merged, decompressed zkey bytes (free with zkp_buffer_free). */
+zkp_status zkp_zkey_read(const char* path, uint8_t** out, size_t* len);
+zkp_status zkp_zkey_read_chunks(const char* const* paths, int n, uint8_t** out, size_t* len);
+void zkp_buffer_free(uint8_t* p);
+
 /* Load only point slice `part` of `nparts` (contiguous ranges of the witness-indexed
  * sections 5-8 and of section 9) onto one device.  Such a prover computes partial sums
  * only (zkp_prove_partial); the quotient is computed in full on every part. */

@@ -95,3 +95,15 @@ def test_gpu_proof_calldata_accepted(golden_dir):
     z = binfile.read_zkey(zk)
     proof, pub = zkp_amd.Prover(zk).prove_raw(wt)
     assert groth16.verify_calldata(z, zkp_amd.solidity_calldata(proof, pub))
+
+
+def test_prove_from_chunked_gz_zkey(golden_dir, tmp_path):
+    """The app's circuit.zkey{b..k}.gz chunks load straight into the prover (§8f row 2)."""
+    import gzip
+    zk, wt = _files(golden_dir, "small")
+    step = (len(zk) + 9) // 10
+    for i, s in enumerate("bcdefghijk"):
+        (tmp_path / ("circuit.zkey%s.gz" % s)).write_bytes(gzip.compress(zk[i * step:(i + 1) * step]))
+    man = json.load(open(os.path.join(golden_dir, "manifest.json")))["circuits"]["small"]
+    res = zkp_amd.Prover(str(tmp_path / "circuit.zkey")).prove(wt, r=int(man["r"]), s=int(man["s"]))
+    assert groth16.js_stringify(res["proof"]) == open(os.path.join(golden_dir, "proof_small.json")).read()

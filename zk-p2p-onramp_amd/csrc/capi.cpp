@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdlib>
+#include <algorithm>
 #include <cstring>
 #include <fstream>
 #include <new>
@@ -13,6 +15,7 @@
 #include "hip_check.hpp"
 #include "host_ec.hpp"
 #include "prover.hpp"
+#include "zkey_io.hpp"
 
 static_assert(sizeof(zkp_partial) == 392, "zkp_partial is exchanged as 392 raw bytes");
 
@@ -153,10 +156,42 @@ zkp_status zkp_prover_load_mem(const uint8_t* zkey, size_t len, const int* devic
 zkp_status zkp_prover_load_file(const char* path, const int* devices, int ndev, zkp_prover** out) {
   if (!path || !out) return fail(ZKP_ERR_INVALID_ARG, "null argument");
   std::vector<uint8_t> buf;
-  zkp_status s = guard([&] { buf = read_file(path); });
+  zkp_status s = guard([&] { buf = zkp::read_zkey_source(path); });
   if (s != ZKP_OK) return s;
   return zkp_prover_load_mem(buf.data(), buf.size(), devices, ndev, out);
 }
+
+zkp_status zkp_prover_load_chunks(const char* const* paths, int n, const int* devices, int ndev, zkp_prover** out) {
+  if (!paths || n < 1 || !out) return fail(ZKP_ERR_INVALID_ARG, "bad argument");
+  std::vector<uint8_t> buf;
+  zkp_status s = guard([&] { buf = zkp::read_zkey_chunks(std::vector<std::string>(paths, paths + n)); });
+  if (s != ZKP_OK) return s;
+  return zkp_prover_load_mem(buf.data(), buf.size(), devices, ndev, out);
+}
+
+static zkp_status hand_out(std::vector<uint8_t>&& v, uint8_t** out, size_t* len) {
+  *out = static_cast<uint8_t*>(std::malloc(std::max<size_t>(v.size(), 1)));
+  if (!*out) return fail(ZKP_ERR_OUT_OF_MEMORY, "host out of memory");
+  std::memcpy(*out, v.data(), v.size());
+  *len = v.size();
+  return ZKP_OK;
+}
+
+zkp_status zkp_zkey_read(const char* path, uint8_t** out, size_t* len) {
+  if (!path || !out || !len) return fail(ZKP_ERR_INVALID_ARG, "null argument");
+  std::vector<uint8_t> buf;
+  zkp_status s = guard([&] { buf = zkp::read_zkey_source(path); });
+  return s != ZKP_OK ? s : hand_out(std::move(buf), out, len);
+}
+
+zkp_status zkp_zkey_read_chunks(const char* const* paths, int n, uint8_t** out, size_t* len) {
+  if (!paths || n < 1 || !out || !len) return fail(ZKP_ERR_INVALID_ARG, "bad argument");
+  std::vector<uint8_t> buf;
+  zkp_status s = guard([&] { buf = zkp::read_zkey_chunks(std::vector<std::string>(paths, paths + n)); });
+  return s != ZKP_OK ? s : hand_out(std::move(buf), out, len);
+}
+
+void zkp_buffer_free(uint8_t* p) { std::free(p); }
 
 zkp_status zkp_prover_load_part(const uint8_t* zkey, size_t len, int device, int part, int nparts,
                                 zkp_prover** out) {

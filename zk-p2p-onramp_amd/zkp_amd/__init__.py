@@ -103,6 +103,13 @@ def load_library(path: str = LIB_PATH):
                                 ctypes.POINTER(ctypes.c_int)]
         lib.zkp_prover_msm_config.argtypes = [P, ctypes.POINTER(ctypes.c_double), ctypes.c_int]
         lib.zkp_proof_calldata.argtypes = [ctypes.POINTER(_Proof), ctypes.c_char_p, sz, ctypes.POINTER(sz)]
+        lib.zkp_prover_load_chunks.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.c_int,
+                                                ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.POINTER(P)]
+        lib.zkp_zkey_read.argtypes = [ctypes.c_char_p, ctypes.POINTER(u8p), ctypes.POINTER(sz)]
+        lib.zkp_zkey_read_chunks.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.c_int, ctypes.POINTER(u8p),
+                                             ctypes.POINTER(sz)]
+        lib.zkp_buffer_free.argtypes = [u8p]
+        lib.zkp_buffer_free.restype = None
         lib.zkp_prover_load_part.argtypes = [u8p, sz, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(P)]
         lib.zkp_prove_partial.argtypes = [P, u8p, sz, ctypes.c_char_p]
         lib.zkp_prove_partial_staged.argtypes = [P, ctypes.c_int, ctypes.c_char_p]
@@ -113,7 +120,8 @@ def load_library(path: str = LIB_PATH):
                      "zkp_prover_timings", "zkp_msm_g1", "zkp_msm_g2", "zkp_ntt_fr", "zkp_quotient",
                      "zkp_witness_stage", "zkp_prove_staged", "zkp_prover_instrument", "zkp_prover_kernel_stats",
                      "zkp_bench_msm", "zkp_bench_ntt", "zkp_msm", "zkp_prover_msm_config",
-                     "zkp_prover_load_part", "zkp_prove_partial", "zkp_proof_calldata", "zkp_prove_partial_staged", "zkp_proof_combine"):
+                     "zkp_prover_load_part", "zkp_prove_partial", "zkp_proof_calldata",
+                     "zkp_prover_load_chunks", "zkp_zkey_read", "zkp_zkey_read_chunks", "zkp_prove_partial_staged", "zkp_proof_combine"):
             getattr(lib, name).restype = ctypes.c_int
         _lib = lib
         return lib
@@ -400,6 +408,23 @@ def proof_combine_raw(zkey, partials, wtns: bytes, r=None, s=None):
     if pr.n_public > npub:
         raise ZkpError(1, "more than %d public signals" % npub)
     return _unpack_proof(pr, pub)
+
+
+def read_zkey(path_or_chunks) -> bytes:
+    """Decompressed, merged zkey bytes (host only): a path (plain or gzip; else path.gz;
+    else the chunks path{a..z}[.gz], the app's circuit.zkey{b..k}.gz) or a list of chunk paths."""
+    lib = load_library()
+    out = ctypes.POINTER(ctypes.c_uint8)()
+    n = ctypes.c_size_t()
+    if isinstance(path_or_chunks, (list, tuple)):
+        arr = (ctypes.c_char_p * len(path_or_chunks))(*[os.fsencode(p) for p in path_or_chunks])
+        _check(lib.zkp_zkey_read_chunks(arr, len(path_or_chunks), ctypes.byref(out), ctypes.byref(n)))
+    else:
+        _check(lib.zkp_zkey_read(os.fsencode(path_or_chunks), ctypes.byref(out), ctypes.byref(n)))
+    try:
+        return ctypes.string_at(out, n.value)
+    finally:
+        lib.zkp_buffer_free(out)
 
 
 def solidity_calldata(proof, public_signals) -> str:
