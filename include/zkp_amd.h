@@ -83,6 +83,14 @@ zkp_status zkp_zkey_read(const char* path, uint8_t** out, size_t* len);
 zkp_status zkp_zkey_read_chunks(const char* const* paths, int n, uint8_t** out, size_t* len);
 void zkp_buffer_free(uint8_t* p);
 
+/* Setup acceleration: the group arithmetic of a phase-2 contribution (`snarkjs zkey
+ * contribute` / `zkey beacon`, reference dizkus-scripts/3_gen_chunk_zkey.sh:27,36) with
+ * secret k (32-byte LE, nonzero mod r) on `device`: delta1, delta2 x k (section 2), every
+ * L (section 8) and H (section 9) point x k^-1.  Section 10 (the contribution
+ * transcript) is copied unchanged.  *out: the new zkey (free with zkp_buffer_free). */
+zkp_status zkp_zkey_contribute(int device, const uint8_t* zkey, size_t len, const uint8_t* k32, uint8_t** out,
+                               size_t* out_len);
+
 /* Load only point slice `part` of `nparts` (contiguous ranges of the witness-indexed
  * sections 5-8 and of section 9) onto one device.  Such a prover computes partial sums
  * only (zkp_prove_partial); the quotient is computed in full on every part. */

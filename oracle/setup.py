@@ -155,3 +155,21 @@ def vkey_json(z: ZKey) -> dict:
         "vk_alphabeta_12": bn254.f12_to_obj(bn254.pairing_snarkjs(z.alpha1, z.beta2)),
         "IC": [g1o(p) for p in z.ic],
     }
+
+
+def contribute_delta(z: ZKey, k: int) -> ZKey:
+    """Group arithmetic of a phase-2 contribution with secret k (snarkjs `zkey contribute`
+    / `zkey beacon`, reference dizkus-scripts/3_gen_chunk_zkey.sh:27,36): delta -> k*delta,
+    so delta1, delta2 are multiplied by k and the L (C) and H sections, which carry
+    delta^-1, by k^-1.  The contribution transcript (section 10) is not modelled."""
+    import copy
+    k %= bn254.R
+    if k == 0:
+        raise ValueError("contribution scalar must be nonzero mod r")
+    ki = bn254.inv(k, bn254.R)
+    out = copy.copy(z)
+    out.delta1 = bn254.g1_mul(z.delta1, k)
+    out.delta2 = bn254.g2_mul(z.delta2, k)
+    out.c = [None if p is None else bn254.g1_mul(p, ki) for p in z.c]
+    out.h = [None if p is None else bn254.g1_mul(p, ki) for p in z.h]
+    return out

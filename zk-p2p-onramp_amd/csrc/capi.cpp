@@ -193,6 +193,14 @@ zkp_status zkp_zkey_read_chunks(const char* const* paths, int n, uint8_t** out, 
 
 void zkp_buffer_free(uint8_t* p) { std::free(p); }
 
+zkp_status zkp_zkey_contribute(int device, const uint8_t* zkey, size_t len, const uint8_t* k32, uint8_t** out,
+                               size_t* out_len) {
+  if (!zkey || !k32 || !out || !out_len) return fail(ZKP_ERR_INVALID_ARG, "null argument");
+  std::vector<uint8_t> buf;
+  zkp_status s = guard([&] { buf = zkp::zkey_apply_delta(device, zkey, len, k32); });
+  return s != ZKP_OK ? s : hand_out(std::move(buf), out, out_len);
+}
+
 zkp_status zkp_prover_load_part(const uint8_t* zkey, size_t len, int device, int part, int nparts,
                                 zkp_prover** out) {
   if (!zkey || !out) return fail(ZKP_ERR_INVALID_ARG, "null argument");

@@ -106,6 +106,9 @@ class Prover {
 void proof_combine(const uint8_t* zkey, size_t len, const zkp_partial* parts, int nparts, const uint8_t* wtns,
                    size_t wlen, const uint8_t* r32, const uint8_t* s32, zkp_proof* out);
 
+// phase-2 contribution math on the GPU (setup.hip): delta -> k*delta
+std::vector<uint8_t> zkey_apply_delta(int device, const uint8_t* zkey, size_t len, const uint8_t* k32);
+
 // kernel-level helpers (C-ABI zkp_msm_g1/g2, zkp_ntt_fr)
 // c / depth: window bits and base-table depth (0 = automatic, as the prover)
 void msm_points(int device, Curve curve, const uint8_t* points, const uint8_t* scalars, size_t n, uint8_t* out,

@@ -108,6 +108,7 @@ def load_library(path: str = LIB_PATH):
         lib.zkp_zkey_read.argtypes = [ctypes.c_char_p, ctypes.POINTER(u8p), ctypes.POINTER(sz)]
         lib.zkp_zkey_read_chunks.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.c_int, ctypes.POINTER(u8p),
                                              ctypes.POINTER(sz)]
+        lib.zkp_zkey_contribute.argtypes = [ctypes.c_int, u8p, sz, u8p, ctypes.POINTER(u8p), ctypes.POINTER(sz)]
         lib.zkp_buffer_free.argtypes = [u8p]
         lib.zkp_buffer_free.restype = None
         lib.zkp_prover_load_part.argtypes = [u8p, sz, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(P)]
@@ -121,7 +122,7 @@ def load_library(path: str = LIB_PATH):
                      "zkp_witness_stage", "zkp_prove_staged", "zkp_prover_instrument", "zkp_prover_kernel_stats",
                      "zkp_bench_msm", "zkp_bench_ntt", "zkp_msm", "zkp_prover_msm_config",
                      "zkp_prover_load_part", "zkp_prove_partial", "zkp_proof_calldata",
-                     "zkp_prover_load_chunks", "zkp_zkey_read", "zkp_zkey_read_chunks", "zkp_prove_partial_staged", "zkp_proof_combine"):
+                     "zkp_prover_load_chunks", "zkp_zkey_read", "zkp_zkey_read_chunks", "zkp_zkey_contribute", "zkp_prove_partial_staged", "zkp_proof_combine"):
             getattr(lib, name).restype = ctypes.c_int
         _lib = lib
         return lib
@@ -421,6 +422,20 @@ def read_zkey(path_or_chunks) -> bytes:
         _check(lib.zkp_zkey_read_chunks(arr, len(path_or_chunks), ctypes.byref(out), ctypes.byref(n)))
     else:
         _check(lib.zkp_zkey_read(os.fsencode(path_or_chunks), ctypes.byref(out), ctypes.byref(n)))
+    try:
+        return ctypes.string_at(out, n.value)
+    finally:
+        lib.zkp_buffer_free(out)
+
+
+def zkey_contribute(zkey: bytes, k: int, device: int = 0) -> bytes:
+    """Phase-2 contribution math on the GPU: delta -> k*delta (sections 2, 8, 9)."""
+    lib = load_library()
+    zp, zk = _buf(bytes(zkey))
+    kp, kk = _buf(int(k).to_bytes(32, "little"))
+    out = ctypes.POINTER(ctypes.c_uint8)()
+    n = ctypes.c_size_t()
+    _check(lib.zkp_zkey_contribute(device, zp, len(zkey), kp, ctypes.byref(out), ctypes.byref(n)))
     try:
         return ctypes.string_at(out, n.value)
     finally:
