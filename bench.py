@@ -271,8 +271,14 @@ def main():
         "unit": "TMAC/s (32x32->64 v_mad_u64_u32)",
         "frac": round(achieved / peak, 4) if (achieved and peak) else None,
         "traffic": traffic.get("hbm_bytes_per_launch") if traffic else None,
+        "traffic_source": "profiles/pmc_accumulate_r01.json (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, per launch)",
         "algorithmic_work_per_launch": {"mixed_adds": int(adds), "fp_mul_per_add": FPMUL_PER_MADD,
                                         "mac_per_fp_mul": MAC_PER_FPMUL},
+        "valu_issue_frac_pmc": traffic.get("valu_issue_frac") if traffic else None,
+        "note": "integer-multiply (VALU) bound, no MFMA/HBM bound applies (SURVEY.md §8d D3); frac counts the "
+                "algorithmic 136 MAC per Fp mul, the kernel issues ~2.7x that in VALU instructions (29-bit-limb "
+                "FIPS product scanning: 162 mads + carries per mul, plus adds/subs) at valu_issue_frac_pmc of the "
+                "measured issue peak",
         "avg_launch_ms": round(acc_ms, 4),
         "launches_timed": g1["launches"],
         "peak_source": peak_src,

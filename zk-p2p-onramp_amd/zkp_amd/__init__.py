@@ -145,6 +145,14 @@ def _buf(data):
     return ctypes.cast(ctypes.c_char_p(data), ctypes.POINTER(ctypes.c_uint8)), data
 
 
+def _copy_out(ptr, n: int) -> bytes:
+    """bytes of a library buffer (ctypes.string_at takes a C int size: > 2 GiB needs a view)."""
+    if n < (1 << 31) - 1:
+        return ctypes.string_at(ptr, n)
+    addr = ctypes.cast(ptr, ctypes.c_void_p).value
+    return bytes(memoryview((ctypes.c_uint8 * n).from_address(addr)))
+
+
 def _le(b) -> int:
     return int.from_bytes(bytes(b), "little")
 
@@ -423,7 +431,7 @@ def read_zkey(path_or_chunks) -> bytes:
     else:
         _check(lib.zkp_zkey_read(os.fsencode(path_or_chunks), ctypes.byref(out), ctypes.byref(n)))
     try:
-        return ctypes.string_at(out, n.value)
+        return _copy_out(out, n.value)
     finally:
         lib.zkp_buffer_free(out)
 
@@ -431,13 +439,17 @@ def read_zkey(path_or_chunks) -> bytes:
 def zkey_contribute(zkey: bytes, k: int, device: int = 0) -> bytes:
     """Phase-2 contribution math on the GPU: delta -> k*delta (sections 2, 8, 9)."""
     lib = load_library()
-    zp, zk = _buf(bytes(zkey))
+    if hasattr(zkey, "ptr") and hasattr(zkey, "len"):  # library-owned buffer (synth.ZkeyBuffer)
+        zp, zlen, zk = ctypes.cast(zkey.ptr, ctypes.POINTER(ctypes.c_uint8)), zkey.len, None
+    else:
+        zp, zk = _buf(zkey)
+        zlen = len(zkey)
     kp, kk = _buf(int(k).to_bytes(32, "little"))
     out = ctypes.POINTER(ctypes.c_uint8)()
     n = ctypes.c_size_t()
-    _check(lib.zkp_zkey_contribute(device, zp, len(zkey), kp, ctypes.byref(out), ctypes.byref(n)))
+    _check(lib.zkp_zkey_contribute(device, zp, zlen, kp, ctypes.byref(out), ctypes.byref(n)))
     try:
-        return ctypes.string_at(out, n.value)
+        return _copy_out(out, n.value)
     finally:
         lib.zkp_buffer_free(out)
 

@@ -87,7 +87,8 @@ class ZkeyBuffer:
         self.ptr, self.len = ptr, n
 
     def bytes(self) -> bytes:
-        return ctypes.string_at(self.ptr, self.len)
+        from . import _copy_out
+        return _copy_out(self.ptr, self.len)
 
     def __del__(self):
         if getattr(self, "ptr", None):
