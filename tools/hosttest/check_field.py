@@ -39,6 +39,15 @@ def main(n=300):
         x, y, wv = a % (2 * R), b % (2 * R), rnd.randrange(2 * R)
         lines.append("rsubmulr %s %s %s" % (w8(x), w8(y), w8(wv)))
         checks.append(("rsubmulr", lambda v, x=x, y=y, w=wv: v % R == (x - y) * w * inv_rp_r % R and v < 2 * R))
+    edge3 = [0, 1, P - 1, P, 2 * P - 1]
+    triples = [(rnd.randrange(2 * P), rnd.randrange(2 * P), rnd.randrange(2 * P)) for _ in range(n)]
+    triples += [(a, b, c) for a in edge3 for b in edge3 for c in edge3]
+    for a, b, c in triples:
+        lines.append("sub2xq %s %s %s" % (w8(a), w8(b), w8(c)))
+        checks.append(("sub2xq", lambda v, a=a, b=b, c=c: v % P == (a - b - 2 * c) % P and v < 2 * P))
+        x, y, z = a % (2 * R), b % (2 * R), c % (2 * R)
+        lines.append("sub2xr %s %s %s" % (w8(x), w8(y), w8(z)))
+        checks.append(("sub2xr", lambda v, x=x, y=y, z=z: v % R == (x - y - 2 * z) % R and v < 2 * R))
     for z in (0, P):
         lines.append("iszq %s" % w8(z)); checks.append(("iszq", lambda v: v == 1))
     out = subprocess.run([BIN], input="\n".join(lines) + "\n", capture_output=True, text=True).stdout.strip().split("\n")

@@ -24,6 +24,8 @@ int main() {
     else if (o == "lsubsqrq") { Fq a = rdf<FqCfg>(), b = rdf<FqCfg>(); prf(sqr(lsub(a, b))); }
     else if (o == "rsubmulq") { Fq a = rdf<FqCfg>(), b = rdf<FqCfg>(), c = rdf<FqCfg>(); prf(mul(c, rsub(a, b))); }
     else if (o == "rsubmulr") { Fr a = rdf<FrCfg>(), b = rdf<FrCfg>(), c = rdf<FrCfg>(); prf(mul(rsub(a, b), c)); }
+    else if (o == "sub2xq") { Fq a = rdf<FqCfg>(), b = rdf<FqCfg>(), c = rdf<FqCfg>(); prf(sub_2x(a, b, c)); }
+    else if (o == "sub2xr") { Fr a = rdf<FrCfg>(), b = rdf<FrCfg>(), c = rdf<FrCfg>(); prf(sub_2x(a, b, c)); }
     else if (o == "mulr") { Fr a = rdf<FrCfg>(), b = rdf<FrCfg>(); prf(mul(a, b)); }
     else if (o == "canonq") { Fq a = rdf<FqCfg>(); prf(canon(a)); }
     else if (o == "iszq") { Fq a = rdf<FqCfg>(); printf("%d", (int)is_zero(a)); }

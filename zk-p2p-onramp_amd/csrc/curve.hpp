@@ -73,7 +73,7 @@ ZDEV Xyzz<F> xyzz_dbl_aff(const Aff<F>& p) {
   F X2 = sqr(p.x);
   F M = add(dbl(X2), X2);
   Xyzz<F> r;
-  r.x = sub(sqr(M), dbl(S));
+  r.x = sub_2x(sqr(M), f_zero<F>(), S);
   r.y = sub(mul(M, sub(S, r.x)), mul(W, p.y));
   r.zz = V;
   r.zzz = W;
@@ -91,7 +91,7 @@ ZDEV Xyzz<F> xyzz_dbl(const Xyzz<F>& p) {
   F X2 = sqr(p.x);
   F M = add(dbl(X2), X2);
   Xyzz<F> r;
-  r.x = sub(sqr(M), dbl(S));
+  r.x = sub_2x(sqr(M), f_zero<F>(), S);
   r.y = sub(mul(M, sub(S, r.x)), mul(W, p.y));
   r.zz = mul(V, p.zz);
   r.zzz = mul(W, p.zzz);
@@ -130,7 +130,7 @@ ZDEV void xyzz_add_aff(Xyzz<F>& acc, const Aff<F>& q, bool neg = false) {
   }
   F PPP = mul(P, PP);
   F Q = mul(acc.x, PP);
-  F X3 = sub(sub(RR, PPP), dbl(Q));
+  F X3 = sub_2x(RR, PPP, Q);
   F Y3 = sub(mul(R, rsub(Q, X3)), mul(acc.y, PPP));
   acc.zz = mul(acc.zz, PP);
   acc.zzz = mul(acc.zzz, PPP);
@@ -163,7 +163,7 @@ ZDEV void xyzz_add(Xyzz<F>& acc, const Xyzz<F>& q) {
   }
   F PPP = mul(P, PP);
   F Q = mul(U1, PP);
-  F X3 = sub(sub(RR, PPP), dbl(Q));
+  F X3 = sub_2x(RR, PPP, Q);
   F Y3 = sub(mul(R, rsub(Q, X3)), mul(S1, PPP));
   acc.zz = mul(mul(acc.zz, q.zz), PP);
   acc.zzz = mul(mul(acc.zzz, q.zzz), PPP);

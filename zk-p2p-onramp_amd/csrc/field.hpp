@@ -197,6 +197,19 @@ ZDEV Fe<C> rsub(const Fe<C>& a, const Fe<C>& b) {
   return s;
 }
 
+// a - b - 2c for a, b, c < 2m (normalised), result < 2m: one limb pass against 6m in the
+// wide borrow form (low limbs + 2^31, so three subtrahends never borrow), one carry
+// normalisation (value in (0, 8m)), then conditional subtractions of 4m and 2m.  The
+// X3 = R^2 - PPP - 2Q of every XYZZ add in one go (~150 instead of ~250 instructions).
+template <class C>
+ZDEV Fe<C> sub_2x(const Fe<C>& a, const Fe<C>& b, const Fe<C>& c) {
+  Fe<C> s;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) s.v[i] = a.v[i] + C::MOD6_WIDE[i] - b.v[i] - (c.v[i] << 1);
+  normalize(s);
+  return cond_sub(cond_sub(s, C::MOD4), C::MOD2);
+}
+
 template <class C>
 ZDEV Fe<C> dbl(const Fe<C>& a) { return add(a, a); }
 
@@ -334,6 +347,9 @@ ZDEV Fq2 add(const Fq2& a, const Fq2& b) { return Fq2{add(a.c0, b.c0), add(a.c1,
 // (unnormalised) operand is not allowed; a normalised < 4m one is (sums < 6m after add's
 // conditional subtraction, products < 24 m^2 < m R').  sqr() subtracts components, so
 // its operand stays canonical: lsub = sub.
+ZDEV Fq2 sub_2x(const Fq2& a, const Fq2& b, const Fq2& c) {
+  return Fq2{sub_2x(a.c0, b.c0, c.c0), sub_2x(a.c1, b.c1, c.c1)};
+}
 ZDEV Fq2 lsub(const Fq2& a, const Fq2& b) { return Fq2{sub(a.c0, b.c0), sub(a.c1, b.c1)}; }
 ZDEV Fq2 rsub(const Fq2& a, const Fq2& b) { return Fq2{lsub(a.c0, b.c0), lsub(a.c1, b.c1)}; }
 ZDEV Fq2 sub(const Fq2& a, const Fq2& b) { return Fq2{sub(a.c0, b.c0), sub(a.c1, b.c1)}; }
