@@ -206,7 +206,8 @@ def main():
     wit = gen_witnesses(circ, wseeds)
     log("[rank %d] circuit + %d witnesses: %.1fs" % (rank, nw, time.time() - t_setup))
     t0 = time.time()
-    zk = circ.zkey(SETUP_SEED, device=local)
+    # host threads for the synthetic key's QAP evaluation: share the host between the ranks
+    zk = circ.zkey(SETUP_SEED, device=local, threads=max(1, (os.cpu_count() or 8) // max(1, world)))
     log("[rank %d] synthetic zkey (%.2f GB): %.1fs" % (rank, zk.len / 1e9, time.time() - t0))
     t0 = time.time()
     prover = zkp_amd.Prover(zk, devices=[local])
