@@ -44,41 +44,66 @@ __device__ __forceinline__ void stage_roots(uint32_t* __restrict__ ltw, const ui
   }
 }
 
-// b radix-2 DIF stages on the LDS tile (rows natural in, bit-reversed out)
+__device__ __forceinline__ Fr lds_get(const uint32_t* __restrict__ lds, int E, int e) {
+  Fr x;
+#pragma unroll
+  for (int l = 0; l < NL; ++l) x.v[l] = lds[l * E + e];
+  return x;
+}
+__device__ __forceinline__ void lds_put(uint32_t* __restrict__ lds, int E, int e, const Fr& x) {
+#pragma unroll
+  for (int l = 0; l < NL; ++l) lds[l * E + e] = x.v[l];
+}
+__device__ __forceinline__ Fr root(const uint32_t* __restrict__ ltw, uint32_t j) {
+  Fr w;
+#pragma unroll
+  for (int l = 0; l < NL; ++l) w.v[l] = ltw[l * MAX_TW + j];
+  return w;
+}
+// DIF butterfly output d = (x - y) w_j, with w_0 = 1 (x - y only feeds the multiply: raw)
+__device__ __forceinline__ Fr bfly_d(const Fr& x, const Fr& y, const uint32_t* __restrict__ ltw, uint32_t j) {
+  return j ? mul(rsub(x, y), root(ltw, j)) : sub(x, y);
+}
+
+// b radix-2 DIF stages on the LDS tile (rows natural in, bit-reversed out), done two at a
+// time as radix-4 groups in registers (half the LDS traffic and barriers of radix-2):
+// rows r0 + {0, H/2, H, 3H/2} of stage t (span H) and t+1 (span H/2), r0 = grp 2H + i.
 __device__ __forceinline__ void dft_stages(uint32_t* __restrict__ lds, const uint32_t* __restrict__ ltw, int E, int b,
                                            int lc) {
   const uint32_t C = 1u << lc;
-  for (int t = 0; t < b; ++t) {
+  int t = 0;
+  for (; t + 1 < b; t += 2) {
     const int lhalf = b - 1 - t;
+    const uint32_t Hh = 1u << (lhalf - 1);
+    for (int q = threadIdx.x; q < (E >> 2); q += TPB) {
+      const uint32_t col = (uint32_t)q & (C - 1), bq = ((uint32_t)q >> lc) & ((1u << (b - 2)) - 1);
+      const uint32_t bl = (uint32_t)q >> (lc + b - 2);
+      const uint32_t i = bq & (Hh - 1), grp = bq >> (lhalf - 1);
+      const uint32_t r0 = (grp << (lhalf + 1)) | i;
+      const int base = (int)(bl << (b + lc)) + (int)col;
+      const int e0 = base + (int)(r0 << lc), st = (int)(Hh << lc);
+      const Fr x0 = lds_get(lds, E, e0), x1 = lds_get(lds, E, e0 + st), x2 = lds_get(lds, E, e0 + 2 * st),
+               x3 = lds_get(lds, E, e0 + 3 * st);
+      // stage t: (x0, x2) with w_(2H)^i, (x1, x3) with w_(2H)^(i + H/2)
+      const Fr s02 = add(x0, x2), d02 = bfly_d(x0, x2, ltw, i << t);
+      const Fr s13 = add(x1, x3), d13 = bfly_d(x1, x3, ltw, (i + Hh) << t);
+      // stage t+1: (s02, s13) and (d02, d13), both with w_H^i
+      const uint32_t j = i << (t + 1);
+      lds_put(lds, E, e0, add(s02, s13));
+      lds_put(lds, E, e0 + st, bfly_d(s02, s13, ltw, j));
+      lds_put(lds, E, e0 + 2 * st, add(d02, d13));
+      lds_put(lds, E, e0 + 3 * st, bfly_d(d02, d13, ltw, j));
+    }
+    __syncthreads();
+  }
+  if (t < b) {  // odd b: the last radix-2 stage (span 1)
     for (int q = threadIdx.x; q < (E >> 1); q += TPB) {
       const uint32_t col = (uint32_t)q & (C - 1), bq = ((uint32_t)q >> lc) & ((1u << (b - 1)) - 1);
       const uint32_t bl = (uint32_t)q >> (lc + b - 1);
-      const uint32_t grp = bq >> lhalf, i = bq & ((1u << lhalf) - 1);
-      const uint32_t r0 = (grp << (lhalf + 1)) + i, r1 = r0 + (1u << lhalf);
-      const int base = (int)(bl << (b + lc));
-      const int e0 = base + (int)((r0 << lc) + col), e1 = base + (int)((r1 << lc) + col);
-      Fr x, y;
-#pragma unroll
-      for (int l = 0; l < NL; ++l) {
-        x.v[l] = lds[l * E + e0];
-        y.v[l] = lds[l * E + e1];
-      }
-      const Fr s = add(x, y);
-      Fr d;
-      if (i) {
-        Fr w;
-        const uint32_t j = i << t;  // w_(2^(lhalf+1))^i = w_(2^b)^(i 2^t)
-#pragma unroll
-        for (int l = 0; l < NL; ++l) w.v[l] = ltw[l * MAX_TW + j];
-        d = mul(rsub(x, y), w);  // x - y only feeds the multiply: raw subtraction
-      } else {
-        d = sub(x, y);
-      }
-#pragma unroll
-      for (int l = 0; l < NL; ++l) {
-        lds[l * E + e0] = s.v[l];
-        lds[l * E + e1] = d.v[l];
-      }
+      const int e0 = (int)(bl << (b + lc)) + (int)((bq << 1) << lc) + (int)col, e1 = e0 + (int)C;
+      const Fr x = lds_get(lds, E, e0), y = lds_get(lds, E, e1);
+      lds_put(lds, E, e0, add(x, y));
+      lds_put(lds, E, e1, sub(x, y));  // span 1: the root is w_2^0 = 1
     }
     __syncthreads();
   }
