@@ -1,0 +1,31 @@
+#!/usr/bin/env python3
+"""Concurrent-stream timeline of one proof from a rocprofv3 kernel trace of bench.py:
+kernels longer than 0.2 ms with start/end offsets, and how much of the proof span is
+covered by the saturating kernels (accumulate, NTT, sort).
+usage: timeline.py <run_kernel_trace.csv> [proof_index=2]"""
+import csv, sys
+from summarize import short
+
+
+def main(path, idx=2):
+    tr = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
+    starts = [int(r["Start_Timestamp"]) for r in tr if "k_build_abc" in r["Kernel_Name"]]
+    t0, t1 = starts[idx], starts[idx + 1]
+    rows = [(int(r["Start_Timestamp"]) - t0, int(r["End_Timestamp"]) - t0, short(r["Kernel_Name"]))
+            for r in tr if t0 <= int(r["Start_Timestamp"]) < t1]
+    for s, e, k in rows:
+        if e - s > 200000:
+            print("%8.2f %8.2f %7.2f %s" % (s / 1e6, e / 1e6, (e - s) / 1e6, k))
+    sat = [(s, e) for s, e, k in rows if k.startswith(("k_acc", "k_ntt", "rocprim")) and e - s > 100000]
+    ev = sorted([(s, 1) for s, e in sat] + [(e, -1) for s, e in sat])
+    cur = last = cov = 0
+    for t, d in ev:
+        if cur > 0:
+            cov += t - last
+        cur += d
+        last = t
+    print("proof span %.2f ms, covered by saturating kernels %.2f ms" % ((t1 - t0) / 1e6, cov / 1e6))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 2)

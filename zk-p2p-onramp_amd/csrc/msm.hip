@@ -170,19 +170,26 @@ hipError_t sort_pairs(void* tmp, size_t& tmp_bytes, const uint32_t* kin, uint32_
 inline size_t level_bound(size_t bound, int S2) { return 2 * bound / S2 + 1; }
 
 template <class F>
-void run_engine(const MsmPlan& plan, const MsmBases& bases, uint32_t* part_a, uint32_t* part_b, uint32_t* buckets,
-                uint32_t* seg_s, uint32_t* seg_t, uint32_t* const sub[2], uint32_t* d_out, hipStream_t st,
-                hipEvent_t ev0, hipEvent_t ev1) {
+void run_accumulate(const MsmPlan& plan, const MsmBases& bases, uint32_t* part_a, hipStream_t st, hipEvent_t ev0,
+                    hipEvent_t ev1) {
   const MsmParams& prm = plan.params();
   const uint32_t nb = (uint32_t)prm.buckets();
-  const uint32_t half = (uint32_t)prm.half();
-  const uint32_t G = (uint32_t)prm.groups;
-  const size_t xyzz_bytes = 16 * (size_t)FWords<F>::W;
   if (ev0) HIPX(hipEventRecord(ev0, st));
   if (plan.entries() > 0)
     hipLaunchKernelGGL(k_accumulate<F>, dim3(grid_for(plan.max_tasks_now())), dim3(TPB), 0, st, bases.data(),
                        plan.vals(), plan.bstart(), plan.bend(), plan.task_off(), nb, (uint32_t)prm.S, part_a);
   if (ev1) HIPX(hipEventRecord(ev1, st));
+  HIPX(hipGetLastError());
+}
+
+template <class F>
+void run_finish(const MsmPlan& plan, uint32_t* part_a, uint32_t* part_b, uint32_t* buckets, uint32_t* seg_s,
+                uint32_t* seg_t, uint32_t* const sub[2], uint32_t* d_out, hipStream_t st) {
+  const MsmParams& prm = plan.params();
+  const uint32_t nb = (uint32_t)prm.buckets();
+  const uint32_t half = (uint32_t)prm.half();
+  const uint32_t G = (uint32_t)prm.groups;
+  const size_t xyzz_bytes = 16 * (size_t)FWords<F>::W;
   size_t bound = plan.max_tasks_now();
   for (int lv = 0; lv < plan.merge_levels() && plan.entries() > 0; ++lv) {
     bound = level_bound(bound, prm.S2);
@@ -376,7 +383,7 @@ void MsmEngine::collect(Stats& s) {
   pending_ = 0;
 }
 
-void MsmEngine::run(const MsmPlan& plan, const MsmBases& bases, uint32_t* d_out) {
+void MsmEngine::accumulate(const MsmPlan& plan, const MsmBases& bases) {
   const MsmParams& p = plan.params();
   if (p.c != prm_.c || p.depth != prm_.depth || p.windows != prm_.windows)
     throw std::runtime_error("MSM: plan and engine parameters differ");
@@ -388,14 +395,27 @@ void MsmEngine::run(const MsmPlan& plan, const MsmBases& bases, uint32_t* d_out)
   const int slot = (instrument_ && pending_ < MAX_PENDING && plan.entries() > 0) ? pending_++ : -1;
   hipEvent_t e0 = slot >= 0 ? ev_[slot][0] : nullptr, e1 = slot >= 0 ? ev_[slot][1] : nullptr;
   if (curve_ == Curve::G1)
-    run_engine<Fq>(plan, bases, part_a_, part_b_, buckets_, seg_s_, seg_t_, sub_, d_out, stream_, e0, e1);
+    run_accumulate<Fq>(plan, bases, part_a_, stream_, e0, e1);
   else
-    run_engine<Fq2>(plan, bases, part_a_, part_b_, buckets_, seg_s_, seg_t_, sub_, d_out, stream_, e0, e1);
+    run_accumulate<Fq2>(plan, bases, part_a_, stream_, e0, e1);
   if (slot >= 0) {
     h_total_[slot] = plan.entries();  // every compacted entry is one mixed addition
     HIPX(hipMemcpyAsync(&h_counts_[slot], plan.task_off() + plan.params().buckets(), 4, hipMemcpyDeviceToHost,
                         stream_));
   }
+}
+
+void MsmEngine::finish(const MsmPlan& plan, uint32_t* d_out, hipStream_t st) {
+  if (!st) st = stream_;
+  if (curve_ == Curve::G1)
+    run_finish<Fq>(plan, part_a_, part_b_, buckets_, seg_s_, seg_t_, sub_, d_out, st);
+  else
+    run_finish<Fq2>(plan, part_a_, part_b_, buckets_, seg_s_, seg_t_, sub_, d_out, st);
+}
+
+void MsmEngine::run(const MsmPlan& plan, const MsmBases& bases, uint32_t* d_out) {
+  accumulate(plan, bases);
+  finish(plan, d_out, stream_);
 }
 
 }  // namespace zkp

@@ -167,6 +167,12 @@ class MsmEngine {
   // everything there; the G group sums (XYZZ, device layout, window_words() words)
   // land in d_out (device).  Nothing is synchronised.
   void run(const MsmPlan& plan, const MsmBases& bases, uint32_t* d_out);
+  // the same in two phases: accumulate() on the engine's stream (bucket-task partial sums),
+  // finish() (merges + reduction + output) on stream `st` (0 = the engine's), which the
+  // caller must order after accumulate(), e.g. by an event; lets a stream run the next
+  // MSM's accumulation while another finishes this one
+  void accumulate(const MsmPlan& plan, const MsmBases& bases);
+  void finish(const MsmPlan& plan, uint32_t* d_out, hipStream_t st = nullptr);
   size_t window_words() const { return (size_t)prm_.groups * prm_.K() * 4 * fwords_; }
 
   // Kernel instrumentation (HIP events on this engine's stream).  When enabled,

@@ -306,6 +306,7 @@ class DevicePipeline {
     HIPX(hipStreamCreateWithPriority(&s0_, hipStreamNonBlocking, prio_hi));
     HIPX(hipStreamCreateWithPriority(&s1_, hipStreamNonBlocking, prio_lo));
     HIPX(hipStreamCreateWithPriority(&s2_, hipStreamNonBlocking, prio_lo));
+    HIPX(hipStreamCreateWithPriority(&s3_, hipStreamNonBlocking, prio_lo));
     for (auto& e : ev_) HIPX(hipEventCreate(&e));
     const ZkeyHeader& h = hdr_;
     const size_t nd_all = h.domain_size, c0 = (size_t)h.n_public + 1;  // first witness index with a C base
@@ -351,10 +352,10 @@ class DevicePipeline {
     // quotient on s0, which then plans and runs the H MSM
     plan_w_ = std::make_unique<MsmPlan>(nv, pw, s2_);
     plan_h_ = std::make_unique<MsmPlan>(nd, ph, s0_);
-    g1a_ = std::make_unique<MsmEngine>(Curve::G1, pw, nv, s2_);
+    for (auto& g : g1w_) g = std::make_unique<MsmEngine>(Curve::G1, pw, nv, s2_);
     g2_ = std::make_unique<MsmEngine>(Curve::G2, pw, nv, s1_);
     g1h_ = std::make_unique<MsmEngine>(Curve::G1, ph, nd, s0_);
-    wina_ = g1a_->window_words();
+    wina_ = g1w_[0]->window_words();
     winh_ = g1h_->window_words();
     win2_ = g2_->window_words();
     HIPX(hipMalloc(&dwin_, win_total() * 4));
@@ -365,7 +366,7 @@ class DevicePipeline {
   ~DevicePipeline() {
     (void)hipSetDevice(dev_);
     ntt_.reset();
-    g1a_.reset();
+    for (auto& g : g1w_) g.reset();
     g1h_.reset();
     g2_.reset();
     plan_w_.reset();
@@ -386,6 +387,7 @@ class DevicePipeline {
     (void)hipStreamDestroy(s0_);
     (void)hipStreamDestroy(s1_);
     (void)hipStreamDestroy(s2_);
+    (void)hipStreamDestroy(s3_);
   }
 
   // witness H2D into dst, bracketed by ev_[0]/ev_[1]
@@ -424,7 +426,7 @@ class DevicePipeline {
 
   void set_instrument(bool on) {
     std::lock_guard<std::mutex> lk(mu_);
-    g1a_->set_instrument(on);
+    for (auto& g : g1w_) g->set_instrument(on);
     g1h_->set_instrument(on);
     g2_->set_instrument(on);
     stats_g1_ = MsmEngine::Stats{};
@@ -476,12 +478,14 @@ class DevicePipeline {
 
   // the whole device pipeline on a resident witness (caller holds mu_, ev_[0..1] recorded)
   MsmOut prove_dev(const uint32_t* d_wit) {
-    // group-sum layout in dwin_: A | B1 | C (engine g1a) | H (g1h) | B2 (g2)
+    // group-sum layout in dwin_: A | B1 | C (engines g1w_) | H (g1h) | B2 (g2)
     uint32_t* wa = dwin_;
     uint32_t* wh = dwin_ + 3 * wina_;
     uint32_t* wb2 = wh + winh_;
-    // s2: witness plan, then G1 MSMs A, B1, C;  s1: G2 MSM B2 on the same plan;
-    // s0: quotient (buildABC, 3 coset NTTs, joinABC), H plan, H MSM.
+    // s2: witness plan, then the G1 accumulations A, B1, C back to back; s3 finishes each
+    // (merges + reduction: latency-bound chains) while s2 accumulates the next;
+    // s1: G2 MSM B2 on the same plan; s0: quotient (buildABC, 3 coset NTTs, joinABC),
+    // H plan, H MSM.
     // MsmPlan::build blocks its host thread once (the sort needs the nonzero-digit
     // count), so each stream is fed from its own host thread; the G2 thread starts
     // once the witness plan is enqueued (its stream then waits on plan.ready()).
@@ -498,10 +502,14 @@ class DevicePipeline {
         plan_w_->build(d_wit + wlo_ * 8, whi_ - wlo_);
         planned.set_value();
         planned_set = true;
-        g1a_->run(*plan_w_, *ta_, wa);
-        g1a_->run(*plan_w_, *tb1_, wa + wina_);
-        g1a_->run(*plan_w_, *tc_, wa + 2 * wina_);
-        HIPX(hipEventRecord(ev_[8], s2_));
+        const MsmBases* tabs[3] = {ta_.get(), tb1_.get(), tc_.get()};
+        for (int m = 0; m < 3; ++m) {
+          g1w_[m]->accumulate(*plan_w_, *tabs[m]);
+          HIPX(hipEventRecord(ev_[10 + m], s2_));
+          HIPX(hipStreamWaitEvent(s3_, ev_[10 + m], 0));
+          g1w_[m]->finish(*plan_w_, wa + m * wina_, s3_);
+        }
+        HIPX(hipEventRecord(ev_[8], s3_));
       } catch (...) {
         err[0] = std::current_exception();
         if (!planned_set) planned.set_exception(std::current_exception());
@@ -550,11 +558,11 @@ class DevicePipeline {
     HIPX(hipMemcpyAsync(hwin_, dwin_, win_total() * 4, hipMemcpyDeviceToHost, s0_));
     HIPX(hipEventRecord(ev_[5], s0_));
     HIPX(hipStreamSynchronize(s0_));
-    g1a_->collect(stats_g1_);
+    for (auto& g : g1w_) g->collect(stats_g1_);
     g1h_->collect(stats_g1_);
     g2_->collect(stats_g2_);
     MsmOut o;
-    const MsmParams& pa = g1a_->params();
+    const MsmParams& pa = g1w_[0]->params();
     const MsmParams& ph = g1h_->params();
     o.a = msm_fold<HFq>(hwin_, pa);
     o.b1 = msm_fold<HFq>(hwin_ + wina_, pa);
@@ -575,8 +583,8 @@ class DevicePipeline {
   size_t wlo_ = 0, whi_ = 0, hlo_ = 0, hhi_ = 0;  // witness / domain slice held by this pipeline
   bool serial_ = std::getenv("ZKP_SERIAL") && std::getenv("ZKP_SERIAL")[0] == '1';  // profiling: no stream overlap
   ZkeyHeader hdr_;
-  hipStream_t s0_ = nullptr, s1_ = nullptr, s2_ = nullptr;
-  hipEvent_t ev_[12];
+  hipStream_t s0_ = nullptr, s1_ = nullptr, s2_ = nullptr, s3_ = nullptr;
+  hipEvent_t ev_[16];
   std::unique_ptr<MsmBases> ta_, tb1_, tc_, tb2_, th_;
   uint32_t* rowptr_[2] = {nullptr, nullptr};
   uint32_t* col_[2] = {nullptr, nullptr};
@@ -586,7 +594,7 @@ class DevicePipeline {
   uint32_t* pscal_ = nullptr;
   std::unique_ptr<NttEngine> ntt_;
   std::unique_ptr<MsmPlan> plan_w_, plan_h_;
-  std::unique_ptr<MsmEngine> g1a_, g1h_, g2_;
+  std::unique_ptr<MsmEngine> g1w_[3], g1h_, g2_;  // g1w_: A, B1, C
   size_t wina_ = 0, winh_ = 0, win2_ = 0;
   size_t win_total() const { return 3 * wina_ + winh_ + win2_; }
   uint32_t* dwin_ = nullptr;
