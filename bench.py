@@ -182,6 +182,8 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("ZKP_BENCH_DEVICE"):  # rehearsal only: put every rank on one GPU
+        local = int(os.environ["ZKP_BENCH_DEVICE"])
     dist = None
     if args.mode == "split":
         if world > 1:

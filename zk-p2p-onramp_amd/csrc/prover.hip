@@ -260,9 +260,20 @@ static int env_int(const char* name, int dflt) {
 // table depth = W (one bucket set) unless the tables would not fit in half of the free
 // HBM, then the largest depth that does (ZKP_TABLE_DEPTH overrides).
 static void choose_msm_params(size_t n_w, size_t n_h, MsmParams& pw, MsmParams& ph) {
+  // measured on the Venmo shape (tools/gpu/sweep_c2.sh): the witness MSMs (70 % of the digits
+  // of a 0/1-heavy witness are single entries) prefer one bit less than lg n - 4, the
+  // uniform-scalar H MSM one bit more (fewer windows; the bucket reduction is cheap)
+  auto lg = [](size_t n) {
+    int l = 0;
+    while ((size_t(1) << l) < n) ++l;
+    return l;
+  };
+  auto clampc = [](int c) { return c < 8 ? 8 : (c > 20 ? 20 : c); };
   const int c = env_int("ZKP_WINDOW_BITS", 0), d = env_int("ZKP_TABLE_DEPTH", 0);
-  pw = MsmParams::make(n_w, c, d);
-  ph = MsmParams::make(n_h, c, d);
+  const int cw = env_int("ZKP_WINDOW_BITS_W", c ? c : clampc(lg(n_w) - 5));
+  const int ch = env_int("ZKP_WINDOW_BITS_H", c ? c : clampc(lg(n_h) - 3));
+  pw = MsmParams::make(n_w, cw, d);
+  ph = MsmParams::make(n_h, ch, d);
   if (d > 0) return;
   size_t free_b = 0, total_b = 0;
   HIPX(hipMemGetInfo(&free_b, &total_b));
@@ -271,8 +282,8 @@ static void choose_msm_params(size_t n_w, size_t n_h, MsmParams& pw, MsmParams& 
   int depth = std::max(pw.windows, ph.windows);
   while (depth > 1 && (size_t)std::min(depth, pw.windows) * row_w + (size_t)std::min(depth, ph.windows) * row_h > budget)
     --depth;
-  pw = MsmParams::make(n_w, c, depth);
-  ph = MsmParams::make(n_h, c, depth);
+  pw = MsmParams::make(n_w, cw, depth);
+  ph = MsmParams::make(n_h, ch, depth);
 }
 
 // upload `count` zkey points (snarkjs LEM layout) into row 0 of a base table at point
