@@ -48,6 +48,13 @@ def main(n=300):
         x, y, z = a % (2 * R), b % (2 * R), c % (2 * R)
         lines.append("sub2xr %s %s %s" % (w8(x), w8(y), w8(z)))
         checks.append(("sub2xr", lambda v, x=x, y=y, z=z: v % R == (x - y - 2 * z) % R and v < 2 * R))
+    # lazily reduced sums of products (field.hpp mul2): a, b < 4m; c, d <= 2m
+    quads = [(rnd.randrange(4 * P), rnd.randrange(4 * P), rnd.randrange(2 * P + 1), rnd.randrange(2 * P + 1))
+             for _ in range(n)]
+    quads += [(4 * P - 1, 4 * P - 1, 2 * P, 2 * P), (0, 0, 0, 0), (4 * P - 1, 1, 2 * P, 2 * P - 1)]
+    for a, b, c, d in quads:
+        lines.append("mul2q %s %s %s %s" % (w8(a), w8(b), w8(c), w8(d)))
+        checks.append(("mul2q", lambda v, a=a, b=b, c=c, d=d: v % P == (a * b + c * d) * inv_rp_p % P and v < 2 * P))
     for z in (0, P):
         lines.append("iszq %s" % w8(z)); checks.append(("iszq", lambda v: v == 1))
     out = subprocess.run([BIN], input="\n".join(lines) + "\n", capture_output=True, text=True).stdout.strip().split("\n")

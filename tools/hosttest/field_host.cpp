@@ -26,6 +26,11 @@ int main() {
     else if (o == "rsubmulr") { Fr a = rdf<FrCfg>(), b = rdf<FrCfg>(), c = rdf<FrCfg>(); prf(mul(rsub(a, b), c)); }
     else if (o == "sub2xq") { Fq a = rdf<FqCfg>(), b = rdf<FqCfg>(), c = rdf<FqCfg>(); prf(sub_2x(a, b, c)); }
     else if (o == "sub2xr") { Fr a = rdf<FrCfg>(), b = rdf<FrCfg>(), c = rdf<FrCfg>(); prf(sub_2x(a, b, c)); }
+    else if (o == "mul2q") { Fq a = rdf<FqCfg>(), b = rdf<FqCfg>(), c = rdf<FqCfg>(), d = rdf<FqCfg>(); prf(mul2(a, b, c, d)); }
+    else if (o == "mul2f2") {  // Fq2: (a0+a1 u)(b0+b1 u) + (c0+c1 u)(d0+d1 u); prints c0 then c1
+      Fq2 a{rdf<FqCfg>(), rdf<FqCfg>()}, b{rdf<FqCfg>(), rdf<FqCfg>()}, c{rdf<FqCfg>(), rdf<FqCfg>()}, d{rdf<FqCfg>(), rdf<FqCfg>()};
+      Fq2 r = mul2(a, b, c, d); prf(r.c0); printf("\n"); prf(r.c1);
+    }
     else if (o == "mulr") { Fr a = rdf<FrCfg>(), b = rdf<FrCfg>(); prf(mul(a, b)); }
     else if (o == "canonq") { Fq a = rdf<FqCfg>(); prf(canon(a)); }
     else if (o == "iszq") { Fq a = rdf<FqCfg>(); printf("%d", (int)is_zero(a)); }

@@ -74,7 +74,7 @@ ZDEV Xyzz<F> xyzz_dbl_aff(const Aff<F>& p) {
   F M = add(dbl(X2), X2);
   Xyzz<F> r;
   r.x = sub_2x(sqr(M), f_zero<F>(), S);
-  r.y = sub(mul(M, sub(S, r.x)), mul(W, p.y));
+  r.y = mul2(M, lsub(S, r.x), W, lsub(f_zero<F>(), p.y));  // M (S - X3) - W Y
   r.zz = V;
   r.zzz = W;
   return r;
@@ -92,7 +92,7 @@ ZDEV Xyzz<F> xyzz_dbl(const Xyzz<F>& p) {
   F M = add(dbl(X2), X2);
   Xyzz<F> r;
   r.x = sub_2x(sqr(M), f_zero<F>(), S);
-  r.y = sub(mul(M, sub(S, r.x)), mul(W, p.y));
+  r.y = mul2(M, lsub(S, r.x), W, lsub(f_zero<F>(), p.y));  // M (S - X3) - W Y
   r.zz = mul(V, p.zz);
   r.zzz = mul(W, p.zzz);
   return r;
@@ -131,7 +131,7 @@ ZDEV void xyzz_add_aff(Xyzz<F>& acc, const Aff<F>& q, bool neg = false) {
   F PPP = mul(P, PP);
   F Q = mul(acc.x, PP);
   F X3 = sub_2x(RR, PPP, Q);
-  F Y3 = sub(mul(R, rsub(Q, X3)), mul(acc.y, PPP));
+  F Y3 = mul2(R, lsub(Q, X3), acc.y, lsub(f_zero<F>(), PPP));  // R (Q - X3) - Y1 PPP
   acc.zz = mul(acc.zz, PP);
   acc.zzz = mul(acc.zzz, PPP);
   acc.x = X3;
@@ -164,7 +164,7 @@ ZDEV void xyzz_add(Xyzz<F>& acc, const Xyzz<F>& q) {
   F PPP = mul(P, PP);
   F Q = mul(U1, PP);
   F X3 = sub_2x(RR, PPP, Q);
-  F Y3 = sub(mul(R, rsub(Q, X3)), mul(S1, PPP));
+  F Y3 = mul2(R, lsub(Q, X3), S1, lsub(f_zero<F>(), PPP));  // R (Q - X3) - S1 PPP
   acc.zz = mul(mul(acc.zz, q.zz), PP);
   acc.zzz = mul(mul(acc.zzz, q.zzz), PPP);
   acc.x = X3;

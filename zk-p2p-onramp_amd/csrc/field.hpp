@@ -89,6 +89,46 @@ ZDEV Fe<C> mul(const Fe<C>& a, const Fe<C>& b) {
   return r;
 }
 
+// Montgomery product of a SUM of two products, (a*b + c*d)/2^261 mod m, with ONE
+// reduction ("lazy reduction"): the a*b, c*d and m*MOD partial products of a column
+// accumulate together.  All four operands normalised (limbs < 2^29; column sums
+// <= 27 * 2^58 < 2^63) and a*b + c*d < m*2^261 (~169 m^2) for an output < 2m.  Used for
+// Y3 = R (Q - X3) - Y1 PPP as R*(Q - X3) + Y1*(2m - PPP): one reduction and no
+// subtraction instead of two multiplies and a subtraction (~230 instructions saved).
+template <class C>
+ZDEV Fe<C> mul2(const Fe<C>& a, const Fe<C>& b, const Fe<C>& c, const Fe<C>& d) {
+  uint32_t m[NL];
+  Fe<C> r;
+  uint64_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) {
+#pragma unroll
+    for (int j = 0; j < i; ++j) {
+      acc += (uint64_t)a.v[j] * b.v[i - j];
+      acc += (uint64_t)c.v[j] * d.v[i - j];
+      acc += (uint64_t)m[j] * C::MOD[i - j];
+    }
+    acc += (uint64_t)a.v[i] * b.v[0];
+    acc += (uint64_t)c.v[i] * d.v[0];
+    m[i] = ((uint32_t)acc * C::INV) & LMASK;
+    acc += (uint64_t)m[i] * C::MOD[0];
+    acc >>= LB;
+  }
+#pragma unroll
+  for (int i = NL; i < 2 * NL - 1; ++i) {
+#pragma unroll
+    for (int j = i - NL + 1; j < NL; ++j) {
+      acc += (uint64_t)a.v[j] * b.v[i - j];
+      acc += (uint64_t)c.v[j] * d.v[i - j];
+      acc += (uint64_t)m[j] * C::MOD[i - j];
+    }
+    r.v[i - NL] = (uint32_t)acc & LMASK;
+    acc >>= LB;
+  }
+  r.v[NL - 1] = (uint32_t)acc;
+  return r;
+}
+
 // Squaring: cross products computed once against a doubled operand.
 template <class C>
 ZDEV Fe<C> sqr(const Fe<C>& a) {
@@ -327,6 +367,17 @@ ZDEV Fq2 mul(const Fq2& a, const Fq2& b) {
   Fq t1 = mul(a.c1, b.c1);
   Fq s0 = add(a.c0, a.c1), s1 = add(b.c0, b.c1);
   Fq t2 = mul(s0, s1);
+  Fq2 r;
+  r.c0 = sub(t0, t1);
+  r.c1 = sub(sub(t2, t0), t1);
+  return r;
+}
+
+// a*b + c*d in Fq2 with three lazily reduced Fq sums (Karatsuba on both products)
+ZDEV Fq2 mul2(const Fq2& a, const Fq2& b, const Fq2& c, const Fq2& d) {
+  const Fq t0 = mul2(a.c0, b.c0, c.c0, d.c0);
+  const Fq t1 = mul2(a.c1, b.c1, c.c1, d.c1);
+  const Fq t2 = mul2(add(a.c0, a.c1), add(b.c0, b.c1), add(c.c0, c.c1), add(d.c0, d.c1));
   Fq2 r;
   r.c0 = sub(t0, t1);
   r.c1 = sub(sub(t2, t0), t1);

@@ -519,6 +519,10 @@ class DevicePipeline {
           HIPX(hipEventRecord(ev_[10 + m], s2_));
           HIPX(hipStreamWaitEvent(s3_, ev_[10 + m], 0));
           g1w_[m]->finish(*plan_w_, wa + m * wina_, s3_);
+          if (serial_) {  // profiling: no overlap between the finish and the next accumulation
+            HIPX(hipEventRecord(ev_[13], s3_));
+            HIPX(hipStreamWaitEvent(s2_, ev_[13], 0));
+          }
         }
         HIPX(hipEventRecord(ev_[8], s3_));
       } catch (...) {
