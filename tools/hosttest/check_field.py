@@ -6,7 +6,7 @@ sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", ".."))
 from oracle import bn254
 P, R = bn254.P, bn254.R
 RP = 1 << 261
-BIN = os.path.join(os.path.dirname(__file__), "field_host")
+BIN = os.environ.get("FIELD_HOST_BIN", os.path.join(os.path.dirname(__file__), "field_host"))
 
 def w8(x): return " ".join("%x" % ((x >> (32 * i)) & 0xffffffff) for i in range(8))
 def p8(s): return sum(int(t, 16) << (32 * i) for i, t in enumerate(s.split()[:8]))
@@ -55,6 +55,20 @@ def main(n=300):
     for a, b, c, d in quads:
         lines.append("mul2q %s %s %s %s" % (w8(a), w8(b), w8(c), w8(d)))
         checks.append(("mul2q", lambda v, a=a, b=b, c=c, d=d: v % P == (a * b + c * d) * inv_rp_p % P and v < 2 * P))
+    # Fq2 products and sums of products (field.hpp Fq2 mul / mul2): components < 4m
+    def f2(a0, a1, b0, b1):
+        return (a0 * b0 - a1 * b1), (a0 * b1 + a1 * b0)
+    f2cases = [[rnd.randrange(4 * P) for _ in range(8)] for _ in range(n)]
+    f2cases += [[4 * P - 1] * 8, [0] * 8, [4 * P - 1, 0, 1, 4 * P - 1, 2 * P, 4 * P - 1, 4 * P - 1, 1]]
+    for t in f2cases:
+        lines.append("mulf2 %s" % " ".join(w8(x) for x in t[:4]))
+        lines.append("mul2f2 %s" % " ".join(w8(x) for x in t))
+        e = f2(*t[:4])
+        g = f2(*t[4:])
+        for k in range(2):
+            checks.append(("mulf2", lambda v, x=e[k]: v % P == x * inv_rp_p % P and v < 2 * P))
+        for k in range(2):
+            checks.append(("mul2f2", lambda v, x=e[k] + g[k]: v % P == x * inv_rp_p % P and v < 2 * P))
     for z in (0, P):
         lines.append("iszq %s" % w8(z)); checks.append(("iszq", lambda v: v == 1))
     out = subprocess.run([BIN], input="\n".join(lines) + "\n", capture_output=True, text=True).stdout.strip().split("\n")

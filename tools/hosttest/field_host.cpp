@@ -31,6 +31,10 @@ int main() {
       Fq2 a{rdf<FqCfg>(), rdf<FqCfg>()}, b{rdf<FqCfg>(), rdf<FqCfg>()}, c{rdf<FqCfg>(), rdf<FqCfg>()}, d{rdf<FqCfg>(), rdf<FqCfg>()};
       Fq2 r = mul2(a, b, c, d); prf(r.c0); printf("\n"); prf(r.c1);
     }
+    else if (o == "mulf2") {  // Fq2 (a0+a1 u)(b0+b1 u); prints c0 then c1
+      Fq2 a{rdf<FqCfg>(), rdf<FqCfg>()}, b{rdf<FqCfg>(), rdf<FqCfg>()};
+      Fq2 r = mul(a, b); prf(r.c0); printf("\n"); prf(r.c1);
+    }
     else if (o == "mulr") { Fr a = rdf<FrCfg>(), b = rdf<FrCfg>(); prf(mul(a, b)); }
     else if (o == "canonq") { Fq a = rdf<FqCfg>(); prf(canon(a)); }
     else if (o == "iszq") { Fq a = rdf<FqCfg>(); printf("%d", (int)is_zero(a)); }

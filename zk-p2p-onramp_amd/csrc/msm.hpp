@@ -26,7 +26,7 @@
 //     4. accumulate: one thread per task, mixed XYZZ additions of gathered bases;
 //                 every thread does the same bounded work whatever the scalar
 //                 distribution (0/1-heavy witnesses put most points in one bucket).
-//     5. merge  : buckets with more than S2 task partials are folded by segmented
+//     5. merge  : buckets with more than 2*S2 task partials are folded by segmented
 //                 merge levels that skip the light buckets; one thread per bucket
 //                 sums what is left.
 //     6. reduce : per group, sum_k (k+1) B_k = sum_p T_p + M sum_b 2^b Q_b from
@@ -212,7 +212,7 @@ class MsmEngine {
 inline int msm_merge_levels(size_t max_n, const MsmParams& prm) {
   size_t m = ((max_n ? max_n : 1) * (size_t)prm.depth + prm.S - 1) / prm.S;
   int levels = 0;
-  while (m > (size_t)prm.S2) {
+  while (m > 2 * (size_t)prm.S2) {
     m = (m + prm.S2 - 1) / prm.S2;
     ++levels;
   }

@@ -121,10 +121,10 @@ ZDEV void accumulate(uint32_t t, const uint32_t* __restrict__ points, const uint
   store_xyzz(out, t, acc);
 }
 
-// ---- bucket merge: only "heavy" buckets (more than S2 partials) take merge levels.
+// ---- bucket merge: only "heavy" buckets (more than 2*S2 partials) take merge levels.
 // The partials of bucket b live at [off[b], off[b] + c) of a ping-pong pair of buffers:
 // after k merge levels applied to it, in buffer k&1 (0 = accumulate output) with
-// c = count after k levels.  A level turns c > S2 partials into ceil(c / S2), written
+// c = count after k levels.  A level turns c > 2*S2 partials into ceil(c / S2), written
 // at the same base off[b] of the other buffer; light buckets are never touched.
 
 // partial count of a bucket with c0 task partials after `levels` merge levels, and the
@@ -132,7 +132,7 @@ ZDEV void accumulate(uint32_t t, const uint32_t* __restrict__ points, const uint
 ZDEV uint32_t merged_count(uint32_t c0, uint32_t S2, int levels, int& applied) {
   uint32_t c = c0;
   applied = 0;
-  for (int l = 0; l < levels && c > S2; ++l) {
+  for (int l = 0; l < levels && c > 2 * S2; ++l) {
     c = (c + S2 - 1) / S2;
     ++applied;
   }
@@ -149,7 +149,7 @@ ZDEV void heavy_counts(uint32_t b, const uint32_t* __restrict__ off, uint32_t nb
   }
   int applied;
   const uint32_t c = merged_count(off[b + 1] - off[b], S2, lvl, applied);
-  cnt[b] = (applied == lvl && c > S2) ? (c + S2 - 1) / S2 : 0u;
+  cnt[b] = (applied == lvl && c > 2 * S2) ? (c + S2 - 1) / S2 : 0u;
 }
 
 // merge task t of level lvl: sums <= S2 consecutive partials of one heavy bucket
@@ -169,7 +169,7 @@ ZDEV void merge_heavy(uint32_t t, const uint32_t* __restrict__ src, const uint32
   store_xyzz(dst, off[b] + j, acc);
 }
 
-// one thread per bucket: fold its (<= S2) remaining partials into buckets[b] (infinity if none)
+// one thread per bucket: fold its (<= 2*S2) remaining partials into buckets[b] (infinity if none)
 template <class F>
 ZDEV void merge_final(uint32_t b, const uint32_t* __restrict__ part0, const uint32_t* __restrict__ part1,
                       const uint32_t* __restrict__ off, uint32_t nb, uint32_t S2, int levels,

@@ -317,7 +317,9 @@ class DevicePipeline {
     HIPX(hipStreamCreateWithPriority(&s0_, hipStreamNonBlocking, prio_hi));
     HIPX(hipStreamCreateWithPriority(&s1_, hipStreamNonBlocking, prio_lo));
     HIPX(hipStreamCreateWithPriority(&s2_, hipStreamNonBlocking, prio_lo));
-    HIPX(hipStreamCreateWithPriority(&s3_, hipStreamNonBlocking, prio_lo));
+    // s3 runs every MSM's finish (merges + reduction: short latency-bound launches) at high
+    // priority, so they slip in between the long accumulations instead of queueing behind them
+    HIPX(hipStreamCreateWithPriority(&s3_, hipStreamNonBlocking, prio_hi));
     for (auto& e : ev_) HIPX(hipEventCreate(&e));
     const ZkeyHeader& h = hdr_;
     const size_t nd_all = h.domain_size, c0 = (size_t)h.n_public + 1;  // first witness index with a C base
@@ -505,6 +507,14 @@ class DevicePipeline {
     std::promise<void> planned;
     std::shared_future<void> planned_f = planned.get_future().share();
     bool planned_set = false;
+    // scheduling experiment (ZKP_SCHED=1): the witness MSMs' accumulations wait for the
+    // quotient, so the quotient -> H plan -> H MSM chain gets the GPU first.  Measured: no
+    // gain (33.7 vs 33.5 ms): the proof is bound by the total work, not by the chain, so
+    // the default lets every stream run freely.  Never in the serial profiling mode.
+    const bool gate = !serial_ && sched_gate_;
+    std::promise<void> qdone;
+    std::shared_future<void> qdone_f = qdone.get_future().share();
+    bool qdone_set = false;
     auto g1_job = [&] {
       try {
         HIPX(hipSetDevice(dev_));
@@ -513,6 +523,10 @@ class DevicePipeline {
         plan_w_->build(d_wit + wlo_ * 8, whi_ - wlo_);
         planned.set_value();
         planned_set = true;
+        if (gate) {  // accumulate only once the quotient (head of the critical H chain) is done
+          qdone_f.get();
+          HIPX(hipStreamWaitEvent(s2_, ev_[3], 0));
+        }
         const MsmBases* tabs[3] = {ta_.get(), tb1_.get(), tc_.get()};
         for (int m = 0; m < 3; ++m) {
           g1w_[m]->accumulate(*plan_w_, *tabs[m]);
@@ -535,8 +549,12 @@ class DevicePipeline {
         planned_f.get();
         HIPX(hipSetDevice(dev_));
         if (serial_) HIPX(hipStreamWaitEvent(s1_, ev_[8], 0));
+        if (gate) {
+          qdone_f.get();
+          HIPX(hipStreamWaitEvent(s1_, ev_[3], 0));
+        }
         HIPX(hipEventRecord(ev_[7], s1_));
-        g2_->run(*plan_w_, *tb2_, wb2);
+        g2_->run(*plan_w_, *tb2_, wb2);  // finish on s1 too: s3 is in-order, the G1 finishes must not queue behind it
         HIPX(hipEventRecord(ev_[6], s1_));
       } catch (...) {
         err[1] = std::current_exception();
@@ -546,10 +564,13 @@ class DevicePipeline {
       try {
         if (serial_) HIPX(hipStreamWaitEvent(s0_, ev_[6], 0));
         enqueue_quotient(d_wit);
+        qdone.set_value();
+        qdone_set = true;
         plan_h_->build(pscal_ + hlo_ * 8, hhi_ - hlo_);
         g1h_->run(*plan_h_, *th_, wh);
       } catch (...) {
         err[2] = std::current_exception();
+        if (!qdone_set) qdone.set_exception(std::current_exception());
       }
     };
     if (serial_) {
@@ -597,6 +618,7 @@ class DevicePipeline {
   int dev_;
   size_t wlo_ = 0, whi_ = 0, hlo_ = 0, hhi_ = 0;  // witness / domain slice held by this pipeline
   bool serial_ = std::getenv("ZKP_SERIAL") && std::getenv("ZKP_SERIAL")[0] == '1';  // profiling: no stream overlap
+  bool sched_gate_ = env_int("ZKP_SCHED", 0) != 0;
   ZkeyHeader hdr_;
   hipStream_t s0_ = nullptr, s1_ = nullptr, s2_ = nullptr, s3_ = nullptr;
   hipEvent_t ev_[16];
