@@ -272,8 +272,14 @@ static void choose_msm_params(size_t n_w, size_t n_h, MsmParams& pw, MsmParams& 
   const int c = env_int("ZKP_WINDOW_BITS", 0), d = env_int("ZKP_TABLE_DEPTH", 0);
   const int cw = env_int("ZKP_WINDOW_BITS_W", c ? c : clampc(lg(n_w) - 5));
   const int ch = env_int("ZKP_WINDOW_BITS_H", c ? c : clampc(lg(n_h) - 3));
+  const int sw = env_int("ZKP_TASK_W", 0), sh = env_int("ZKP_TASK_H", 0);  // entries per task (tuning)
+  auto tasks = [&] {
+    if (sw > 0) pw.S = sw;
+    if (sh > 0) ph.S = sh;
+  };
   pw = MsmParams::make(n_w, cw, d);
   ph = MsmParams::make(n_h, ch, d);
+  tasks();
   if (d > 0) return;
   size_t free_b = 0, total_b = 0;
   HIPX(hipMemGetInfo(&free_b, &total_b));
@@ -284,6 +290,7 @@ static void choose_msm_params(size_t n_w, size_t n_h, MsmParams& pw, MsmParams& 
     --depth;
   pw = MsmParams::make(n_w, cw, depth);
   ph = MsmParams::make(n_h, ch, depth);
+  tasks();
 }
 
 // upload `count` zkey points (snarkjs LEM layout) into row 0 of a base table at point
@@ -315,8 +322,28 @@ class DevicePipeline {
     int prio_lo = 0, prio_hi = 0;
     HIPX(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
     HIPX(hipStreamCreateWithPriority(&s0_, hipStreamNonBlocking, prio_hi));
-    HIPX(hipStreamCreateWithPriority(&s1_, hipStreamNonBlocking, prio_lo));
-    HIPX(hipStreamCreateWithPriority(&s2_, hipStreamNonBlocking, prio_lo));
+    // ZKP_RESERVE_CUS = r > 0: the witness-MSM streams s1, s2 run on all CUs but r, so the
+    // critical chain on s0 always finds free CUs: its memory-bound H plan (radix sort)
+    // otherwise gets workgroup slots only as the long accumulation workgroups retire
+    const int reserve = serial_ ? 0 : env_int("ZKP_RESERVE_CUS", 0);
+    hipDeviceProp_t prop;
+    HIPX(hipGetDeviceProperties(&prop, dev_));
+    const int ncu = prop.multiProcessorCount;
+    if (reserve > 0 && reserve < ncu) {
+      std::vector<uint32_t> mask((ncu + 31) / 32, 0);
+      for (int i = 0; i < ncu; ++i)  // r evenly spaced CUs left out
+        if ((int64_t)i * reserve / ncu == (int64_t)(i + 1) * reserve / ncu) mask[i / 32] |= 1u << (i % 32);
+      HIPX(hipExtStreamCreateWithCUMask(&s1_, (uint32_t)mask.size(), mask.data()));
+      HIPX(hipExtStreamCreateWithCUMask(&s2_, (uint32_t)mask.size(), mask.data()));
+      // ... and the H plan (digits + radix sort: memory-bound, and its decoupled look-back
+      // stalls behind any block that shares a CU with the accumulations) runs on just those r
+      for (auto& w : mask) w = ~w;
+      if (ncu % 32) mask.back() &= (1u << (ncu % 32)) - 1;
+      HIPX(hipExtStreamCreateWithCUMask(&s4_, (uint32_t)mask.size(), mask.data()));
+    } else {
+      HIPX(hipStreamCreateWithPriority(&s1_, hipStreamNonBlocking, prio_lo));
+      HIPX(hipStreamCreateWithPriority(&s2_, hipStreamNonBlocking, prio_lo));
+    }
     // s3 runs every MSM's finish (merges + reduction: short latency-bound launches) at high
     // priority, so they slip in between the long accumulations instead of queueing behind them
     HIPX(hipStreamCreateWithPriority(&s3_, hipStreamNonBlocking, prio_hi));
@@ -364,7 +391,7 @@ class DevicePipeline {
     // the witness plan (built on s2) feeds A/B1/C on s2 and B2 on s1; they overlap the
     // quotient on s0, which then plans and runs the H MSM
     plan_w_ = std::make_unique<MsmPlan>(nv, pw, s2_);
-    plan_h_ = std::make_unique<MsmPlan>(nd, ph, s0_);
+    plan_h_ = std::make_unique<MsmPlan>(nd, ph, s4_ ? s4_ : s0_);
     for (auto& g : g1w_) g = std::make_unique<MsmEngine>(Curve::G1, pw, nv, s2_);
     g2_ = std::make_unique<MsmEngine>(Curve::G2, pw, nv, s1_);
     g1h_ = std::make_unique<MsmEngine>(Curve::G1, ph, nd, s0_);
@@ -401,6 +428,7 @@ class DevicePipeline {
     (void)hipStreamDestroy(s1_);
     (void)hipStreamDestroy(s2_);
     (void)hipStreamDestroy(s3_);
+    if (s4_) (void)hipStreamDestroy(s4_);
   }
 
   // witness H2D into dst, bracketed by ev_[0]/ev_[1]
@@ -515,6 +543,9 @@ class DevicePipeline {
     std::promise<void> qdone;
     std::shared_future<void> qdone_f = qdone.get_future().share();
     bool qdone_set = false;
+    std::promise<void> hdone;  // H plan enqueued
+    std::shared_future<void> hdone_f = hdone.get_future().share();
+    bool hdone_set = false;
     auto g1_job = [&] {
       try {
         HIPX(hipSetDevice(dev_));
@@ -526,6 +557,10 @@ class DevicePipeline {
         if (gate) {  // accumulate only once the quotient (head of the critical H chain) is done
           qdone_f.get();
           HIPX(hipStreamWaitEvent(s2_, ev_[3], 0));
+          if (gate_mode_ >= 2) {  // ... and the H plan
+            hdone_f.get();
+            HIPX(hipStreamWaitEvent(s2_, plan_h_->ready(), 0));
+          }
         }
         const MsmBases* tabs[3] = {ta_.get(), tb1_.get(), tc_.get()};
         for (int m = 0; m < 3; ++m) {
@@ -549,9 +584,13 @@ class DevicePipeline {
         planned_f.get();
         HIPX(hipSetDevice(dev_));
         if (serial_) HIPX(hipStreamWaitEvent(s1_, ev_[8], 0));
-        if (gate) {
+        if (gate && gate_mode_ != 3) {  // mode 3: the G2 MSM (longest finish) runs from the start
           qdone_f.get();
           HIPX(hipStreamWaitEvent(s1_, ev_[3], 0));
+          if (gate_mode_ == 2) {
+            hdone_f.get();
+            HIPX(hipStreamWaitEvent(s1_, plan_h_->ready(), 0));
+          }
         }
         HIPX(hipEventRecord(ev_[7], s1_));
         g2_->run(*plan_w_, *tb2_, wb2);  // finish on s1 too: s3 is in-order, the G1 finishes must not queue behind it
@@ -566,11 +605,15 @@ class DevicePipeline {
         enqueue_quotient(d_wit);
         qdone.set_value();
         qdone_set = true;
+        if (s4_) HIPX(hipStreamWaitEvent(s4_, ev_[3], 0));
         plan_h_->build(pscal_ + hlo_ * 8, hhi_ - hlo_);
+        hdone.set_value();
+        hdone_set = true;
         g1h_->run(*plan_h_, *th_, wh);
       } catch (...) {
         err[2] = std::current_exception();
         if (!qdone_set) qdone.set_exception(std::current_exception());
+        if (!hdone_set) hdone.set_exception(std::current_exception());
       }
     };
     if (serial_) {
@@ -618,9 +661,11 @@ class DevicePipeline {
   int dev_;
   size_t wlo_ = 0, whi_ = 0, hlo_ = 0, hhi_ = 0;  // witness / domain slice held by this pipeline
   bool serial_ = std::getenv("ZKP_SERIAL") && std::getenv("ZKP_SERIAL")[0] == '1';  // profiling: no stream overlap
-  bool sched_gate_ = env_int("ZKP_SCHED", 0) != 0;
+  int gate_mode_ = env_int("ZKP_SCHED", 0);
+  bool sched_gate_ = gate_mode_ != 0;
   ZkeyHeader hdr_;
   hipStream_t s0_ = nullptr, s1_ = nullptr, s2_ = nullptr, s3_ = nullptr;
+  hipStream_t s4_ = nullptr;  // H plan on the reserved CUs (ZKP_RESERVE_CUS > 0), else s0
   hipEvent_t ev_[16];
   std::unique_ptr<MsmBases> ta_, tb1_, tc_, tb2_, th_;
   uint32_t* rowptr_[2] = {nullptr, nullptr};
