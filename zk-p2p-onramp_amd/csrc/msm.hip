@@ -103,8 +103,15 @@ __global__ __launch_bounds__(TPB) void k_heavy_counts(const uint32_t* __restrict
                                                       int lvl, uint32_t* __restrict__ cnt) {
   msmk::heavy_counts(blockIdx.x * TPB + threadIdx.x, off, nb, S2, lvl, cnt);
 }
+// G2 (Fq2) accumulation: without a bound the compiler takes 256 VGPRs + AGPRs (one wave
+// per SIMD, nothing to hide the mad-chain latency); two waves per SIMD (a few spilled
+// dwords; measured 5.24 -> 4.55 ms per 6.4 M-point G2 MSM)
 template <class F>
-__global__ __launch_bounds__(TPB) void k_accumulate(const uint32_t* __restrict__ points,
+struct AccWaves {
+  static constexpr int value = FWords<F>::W == 16 ? 2 : 1;
+};
+template <class F>
+__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(AccWaves<F>::value))) void k_accumulate(const uint32_t* __restrict__ points,
                                                     const uint32_t* __restrict__ vals,
                                                     const uint32_t* __restrict__ start,
                                                     const uint32_t* __restrict__ end,
@@ -147,7 +154,8 @@ __global__ __launch_bounds__(TPB) void k_subset_level(const uint32_t* __restrict
 // Bucket-key sort: rocprim onesweep with 9-bit digits (512-way, 2 passes for the 17/18-bit keys
 // of c = 18/19) instead of the default 8-bit (3 passes): measured 35.7 vs 36.1 ms per proof;
 // other key widths keep the default (e.g. 15 bits: 2 passes either way, default faster).
-// ZKP_SORT_BITS=8 forces the default.
+// ZKP_SORT_BITS=8 forces the default.  (A 10-bit config for the H plan's 19-bit keys, 2
+// passes instead of 3, measured slower: 1.6 + 1.45 ms against 3 x 0.73 ms.)
 using SortCfg9 = rocprim::radix_sort_config<
     rocprim::default_config, rocprim::default_config,
     rocprim::radix_sort_onesweep_config<rocprim::kernel_config<256, 12>, rocprim::kernel_config<512, 12>, 9,
