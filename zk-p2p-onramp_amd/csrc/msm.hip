@@ -103,9 +103,10 @@ __global__ __launch_bounds__(TPB) void k_heavy_counts(const uint32_t* __restrict
                                                       int lvl, uint32_t* __restrict__ cnt) {
   msmk::heavy_counts(blockIdx.x * TPB + threadIdx.x, off, nb, S2, lvl, cnt);
 }
-// G2 (Fq2) accumulation: without a bound the compiler takes 256 VGPRs + AGPRs (one wave
-// per SIMD, nothing to hide the mad-chain latency); two waves per SIMD (a few spilled
-// dwords; measured 5.24 -> 4.55 ms per 6.4 M-point G2 MSM)
+// G2 (Fq2) accumulation and bucket merges (the wide finish kernels): without a bound the
+// compiler takes 256 VGPRs + AGPRs (one wave per SIMD, nothing to hide the mad-chain
+// latency); two waves per SIMD (a few spilled dwords; accumulation measured 5.24 -> 4.55 ms
+// per 6.4 M-point G2 MSM)
 template <class F>
 struct AccWaves {
   static constexpr int value = FWords<F>::W == 16 ? 2 : 1;
@@ -120,14 +121,14 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(AccWaves<F>
   msmk::accumulate<F>(blockIdx.x * TPB + threadIdx.x, points, vals, start, end, off, nb, S, out);
 }
 template <class F>
-__global__ __launch_bounds__(TPB) void k_merge_heavy(const uint32_t* __restrict__ src,
+__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(AccWaves<F>::value))) void k_merge_heavy(const uint32_t* __restrict__ src,
                                                      const uint32_t* __restrict__ off,
                                                      const uint32_t* __restrict__ hoff, uint32_t nb, uint32_t S2,
                                                      int lvl, uint32_t* __restrict__ dst) {
   msmk::merge_heavy<F>(blockIdx.x * TPB + threadIdx.x, src, off, hoff, nb, S2, lvl, dst);
 }
 template <class F>
-__global__ __launch_bounds__(TPB) void k_merge_final(const uint32_t* __restrict__ part0,
+__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(AccWaves<F>::value))) void k_merge_final(const uint32_t* __restrict__ part0,
                                                      const uint32_t* __restrict__ part1,
                                                      const uint32_t* __restrict__ off, uint32_t nb, uint32_t S2,
                                                      int levels, uint32_t* __restrict__ buckets) {
