@@ -67,6 +67,26 @@ def test_msm_g1_edge_distributions():
         assert got == want, name
 
 
+def test_msm_g1_bucket_binning(monkeypatch):
+    # the opt-in two-level counting-sort plan (ZKP_PLAN_SORT=bins): skewed (one bucket),
+    # uniform, sparse and multi-group inputs against the oracle
+    monkeypatch.setenv("ZKP_PLAN_SORT", "bins")
+    pts = _pts(300, 41)
+    rng = circuit.SplitMix64(42, 1)
+    uni = [rng.fr() for _ in range(300)]
+    cases = [
+        (pts, uni, 0, 0),
+        (pts, [1] * 150 + uni[:150], 0, 0),          # circuit-like: half the entries in bucket 0
+        (pts, [1] * 300, 8, 0),
+        (pts, uni, 6, 4),                             # 2 bucket groups
+        (pts, [0] * 299 + [5], 0, 0),
+        (pts[:1], [0], 0, 0),
+    ]
+    for p, s, c, d in cases:
+        pb, sb = _blob(p, s)
+        assert zkp_amd.msm_g1(pb, sb, window_bits=c, table_depth=d) == groth16.msm_g1(p, s), (c, d)
+
+
 @pytest.mark.parametrize("k", [1, 4, 10, 12])
 def test_ntt_golden(golden_dir, k):
     d = json.load(open(os.path.join(golden_dir, "ntt_%d.json" % k)))

@@ -107,8 +107,15 @@ __global__ __launch_bounds__(TPB) void k_heavy_counts(const uint32_t* __restrict
 // compiler takes 256 VGPRs + AGPRs (one wave per SIMD, nothing to hide the mad-chain
 // latency); two waves per SIMD (a few spilled dwords; accumulation measured 5.24 -> 4.55 ms
 // per 6.4 M-point G2 MSM)
+#ifndef ZKP_G1_ACC_WAVES
+#define ZKP_G1_ACC_WAVES 1  // 1 = no bound (118 VGPRs, 4 waves); a prefetching gather at 3 or 4 waves measured slower
+#endif
 template <class F>
 struct AccWaves {
+  static constexpr int value = FWords<F>::W == 16 ? 2 : ZKP_G1_ACC_WAVES;
+};
+template <class F>
+struct MergeWaves {
   static constexpr int value = FWords<F>::W == 16 ? 2 : 1;
 };
 template <class F>
@@ -121,14 +128,14 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(AccWaves<F>
   msmk::accumulate<F>(blockIdx.x * TPB + threadIdx.x, points, vals, start, end, off, nb, S, out);
 }
 template <class F>
-__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(AccWaves<F>::value))) void k_merge_heavy(const uint32_t* __restrict__ src,
+__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(MergeWaves<F>::value))) void k_merge_heavy(const uint32_t* __restrict__ src,
                                                      const uint32_t* __restrict__ off,
                                                      const uint32_t* __restrict__ hoff, uint32_t nb, uint32_t S2,
                                                      int lvl, uint32_t* __restrict__ dst) {
   msmk::merge_heavy<F>(blockIdx.x * TPB + threadIdx.x, src, off, hoff, nb, S2, lvl, dst);
 }
 template <class F>
-__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(AccWaves<F>::value))) void k_merge_final(const uint32_t* __restrict__ part0,
+__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(MergeWaves<F>::value))) void k_merge_final(const uint32_t* __restrict__ part0,
                                                      const uint32_t* __restrict__ part1,
                                                      const uint32_t* __restrict__ off, uint32_t nb, uint32_t S2,
                                                      int levels, uint32_t* __restrict__ buckets) {
@@ -173,6 +180,166 @@ hipError_t sort_pairs(void* tmp, size_t& tmp_bytes, const uint32_t* kin, uint32_
   if (sort_bits() == 9 && (end_bit == 17 || end_bit == 18))  // 2 passes of 9 instead of 3 of 8
     return rocprim::radix_sort_pairs<SortCfg9>(tmp, tmp_bytes, kin, kout, vin, vout, n, 0u, (unsigned)end_bit, st);
   return rocprim::radix_sort_pairs(tmp, tmp_bytes, kin, kout, vin, vout, n, 0u, (unsigned)end_bit, st);
+}
+
+// ---- bucket binning (opt-in, ZKP_PLAN_SORT=bins): grouping the nonzero digits by bucket as a
+// two-level counting sort with no decoupled look-back (every workgroup independent, so it
+// keeps its speed beside the long accumulation kernels of other streams, unlike a onesweep
+// radix sort):
+//   k_bin_hist     per (coarse bin = top <= 9 key bits, digit block) counts in LDS
+//   scan           -> every block's write offset inside every coarse bin (bin-major)
+//   k_bin_scatter  recomputes the digits, writes (fine key bits, base|sign) into the bins
+//   k_chunk_*      each bin grouped by its fine key bits (below), bucket bounds on the way
+// Entry order inside a bucket is not fixed (LDS atomics): the bucket sum is the same group
+// element in any order, so the MSM result is unchanged.
+constexpr int BIN_R = 16;          // scalars per thread in the binning passes (long runs per bin)
+constexpr int MAX_COARSE_BITS = 9;
+constexpr int MAX_FINE_BITS = 13;  // 32 KiB LDS histogram
+
+// count (or, with rank != nullptr, claim a slot for) one entry in LDS counter h[b]; lanes of a
+// wave that all hit the same counter (the skewed buckets of 0/1 witness values) use one atomic
+__device__ __forceinline__ uint32_t lds_claim(uint32_t* h, uint32_t b, bool valid) {
+  const uint64_t m = __ballot(valid);
+  if (!m) return 0;
+  const int leader = __builtin_ctzll(m);
+  const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)b, leader);
+  const uint64_t same = __ballot(valid && b == b0);
+  if (same == m) {
+    uint32_t base = 0;
+    if ((int)(threadIdx.x & 63) == leader) base = atomicAdd(&h[b0], (uint32_t)__popcll(m));
+    base = (uint32_t)__builtin_amdgcn_readlane((int)base, leader);
+    return base + lane_rank(m);
+  }
+  return valid ? atomicAdd(&h[b], 1u) : 0u;
+}
+
+__global__ __launch_bounds__(TPB) void k_bin_hist(const uint32_t* __restrict__ scalars, uint32_t n, int c, int W,
+                                                  int T, int fb, uint32_t nbins, uint32_t* __restrict__ hist) {
+  __shared__ uint32_t h[1 << MAX_COARSE_BITS];
+  for (uint32_t b = threadIdx.x; b < nbins; b += TPB) h[b] = 0;
+  __syncthreads();
+  for (int r = 0; r < BIN_R; ++r) {
+    const uint32_t i = (blockIdx.x * BIN_R + r) * TPB + threadIdx.x;
+    const bool active = i < n;
+    uint32_t s[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    if (active) msmk::load_scalar(scalars, i, s);
+    uint32_t carry = 0;
+    for (int w = 0; w < W; ++w) {
+      uint32_t key, val;
+      const bool valid = msmk::digit_entry(s, w, c, T, n, i, carry, key, val) && active;
+      lds_claim(h, key >> fb, valid);
+    }
+  }
+  __syncthreads();
+  for (uint32_t b = threadIdx.x; b < nbins; b += TPB) hist[(size_t)b * gridDim.x + blockIdx.x] = h[b];
+}
+
+__global__ __launch_bounds__(TPB) void k_bin_scatter(const uint32_t* __restrict__ scalars, uint32_t n, int c, int W,
+                                                     int T, int fb, uint32_t nbins, const uint32_t* __restrict__ hoff,
+                                                     uint32_t* __restrict__ fine, uint32_t* __restrict__ vals) {
+  __shared__ uint32_t cur[1 << MAX_COARSE_BITS];
+  for (uint32_t b = threadIdx.x; b < nbins; b += TPB) cur[b] = hoff[(size_t)b * gridDim.x + blockIdx.x];
+  __syncthreads();
+  const uint32_t fmask = (1u << fb) - 1;
+  for (int r = 0; r < BIN_R; ++r) {
+    const uint32_t i = (blockIdx.x * BIN_R + r) * TPB + threadIdx.x;
+    const bool active = i < n;
+    uint32_t s[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    if (active) msmk::load_scalar(scalars, i, s);
+    uint32_t carry = 0;
+    for (int w = 0; w < W; ++w) {
+      uint32_t key, val;
+      const bool valid = msmk::digit_entry(s, w, c, T, n, i, carry, key, val) && active;
+      const uint32_t pos = lds_claim(cur, key >> fb, valid);
+      if (valid) {
+        fine[pos] = key & fmask;
+        vals[pos] = val;
+      }
+    }
+  }
+}
+
+// pass 2 works on chunks of <= BIN_CHUNK entries of one coarse bin (a skewed bin -- the
+// bucket of every witness value 1 -- spreads over many workgroups):
+//   k_chunk_count  chunks per bin;  scan -> choff
+//   k_chunk_hist   per chunk LDS histogram of the fine bits -> hist2[nf*choff[b] + f*nch_b + c]
+//   scan           -> global sorted position of every (bin, fine, chunk) run
+//   k_chunk_scatter / k_chunk_bounds  the entries, and every bucket's [start, end)
+constexpr uint32_t BIN_CHUNK = 16384;
+
+__global__ __launch_bounds__(TPB) void k_chunk_count(const uint32_t* __restrict__ hoff, uint32_t nblk, uint32_t nbins,
+                                                     uint32_t* __restrict__ nch) {
+  const uint32_t b = blockIdx.x * TPB + threadIdx.x;
+  if (b > nbins) return;
+  nch[b] = b == nbins ? 0u
+                      : (hoff[(size_t)(b + 1) * nblk] - hoff[(size_t)b * nblk] + BIN_CHUNK - 1) / BIN_CHUNK;
+}
+
+struct ChunkRange {
+  uint32_t b, c, nch, lo, hi;
+};
+__device__ __forceinline__ bool chunk_range(const uint32_t* __restrict__ hoff, uint32_t nblk,
+                                            const uint32_t* __restrict__ choff, uint32_t nbins, uint32_t id,
+                                            ChunkRange& r) {
+  if (id >= choff[nbins]) return false;
+  r.b = msmk::seg_search(choff, nbins, id);
+  r.c = id - choff[r.b];
+  r.nch = choff[r.b + 1] - choff[r.b];
+  const uint32_t blo = hoff[(size_t)r.b * nblk], bhi = hoff[(size_t)(r.b + 1) * nblk];
+  r.lo = blo + r.c * BIN_CHUNK;
+  r.hi = msmk::umin(bhi, r.lo + BIN_CHUNK);
+  return true;
+}
+
+__global__ __launch_bounds__(TPB) void k_chunk_hist(const uint32_t* __restrict__ fine, const uint32_t* __restrict__ hoff,
+                                                    uint32_t nblk, const uint32_t* __restrict__ choff, uint32_t nbins,
+                                                    int fb, uint32_t* __restrict__ hist2) {
+  __shared__ uint32_t h[1 << MAX_FINE_BITS];
+  ChunkRange r;
+  if (!chunk_range(hoff, nblk, choff, nbins, blockIdx.x, r)) return;
+  const uint32_t nf = 1u << fb;
+  for (uint32_t f = threadIdx.x; f < nf; f += TPB) h[f] = 0;
+  __syncthreads();
+  for (uint32_t j0 = r.lo; j0 < r.hi; j0 += TPB) {
+    const uint32_t j = j0 + threadIdx.x;
+    lds_claim(h, j < r.hi ? fine[j] : 0u, j < r.hi);
+  }
+  __syncthreads();
+  const size_t base = (size_t)nf * choff[r.b] + r.c;
+  for (uint32_t f = threadIdx.x; f < nf; f += TPB) hist2[base + (size_t)f * r.nch] = h[f];
+}
+
+__global__ __launch_bounds__(TPB) void k_chunk_scatter(const uint32_t* __restrict__ fine,
+                                                       const uint32_t* __restrict__ vin,
+                                                       const uint32_t* __restrict__ hoff, uint32_t nblk,
+                                                       const uint32_t* __restrict__ choff, uint32_t nbins, int fb,
+                                                       const uint32_t* __restrict__ hoff2,
+                                                       uint32_t* __restrict__ vout) {
+  __shared__ uint32_t cur[1 << MAX_FINE_BITS];
+  ChunkRange r;
+  if (!chunk_range(hoff, nblk, choff, nbins, blockIdx.x, r)) return;
+  const uint32_t nf = 1u << fb;
+  const size_t base = (size_t)nf * choff[r.b] + r.c;
+  for (uint32_t f = threadIdx.x; f < nf; f += TPB) cur[f] = hoff2[base + (size_t)f * r.nch];
+  __syncthreads();
+  for (uint32_t j0 = r.lo; j0 < r.hi; j0 += TPB) {
+    const uint32_t j = j0 + threadIdx.x;
+    const bool ok = j < r.hi;
+    const uint32_t pos = lds_claim(cur, ok ? fine[j] : 0u, ok);
+    if (ok) vout[pos] = vin[j];
+  }
+}
+
+__global__ __launch_bounds__(TPB) void k_chunk_bounds(const uint32_t* __restrict__ choff, int fb, uint32_t nb,
+                                                      const uint32_t* __restrict__ hoff2, uint32_t* __restrict__ start,
+                                                      uint32_t* __restrict__ end) {
+  const uint32_t k = blockIdx.x * TPB + threadIdx.x;
+  if (k >= nb) return;
+  const uint32_t nf = 1u << fb, b = k >> fb, f = k & (nf - 1);
+  const uint32_t nch = choff[b + 1] - choff[b];
+  const size_t base = (size_t)nf * choff[b];
+  start[k] = hoff2[base + (size_t)f * nch];
+  end[k] = hoff2[base + (size_t)(f + 1) * nch];
 }
 
 // heavy-merge grid bound per level: heavy c > S2  =>  ceil(c/S2) <= 2c/S2
@@ -280,11 +447,35 @@ MsmPlan::MsmPlan(size_t max_n, const MsmParams& prm, hipStream_t stream)
   HIPX(hipMalloc(&bcnt_, ncnt * 4));
   HIPX(hipMalloc(&boff_, ncnt * 4));
   HIPX(hipHostMalloc(&h_valid_, 4, hipHostMallocDefault));
+  {
+    int kb = 0;
+    while ((size_t(1) << kb) < nbuckets_) ++kb;
+    const int coarse = std::min(kb, MAX_COARSE_BITS);
+    fine_bits_ = kb - coarse;
+    nbins_ = (uint32_t)((nbuckets_ + (size_t(1) << fine_bits_) - 1) >> fine_bits_);
+    // opt-in (ZKP_PLAN_SORT=bins): correct, contention-robust, but its register-to-global
+    // scatters are not staged through LDS and measured slower than the radix sort (serial
+    // 5.2 vs 4.0 ms of plan kernels per proof; proof 32.8 vs 31.0 ms)
+    const char* e = std::getenv("ZKP_PLAN_SORT");
+    use_bins_ = fine_bits_ <= MAX_FINE_BITS && e && std::string(e) == "bins";
+    if (use_bins_) {
+      const size_t nh = (size_t)nbins_ * grid_for(max_n_, TPB * BIN_R) + 1;
+      HIPX(hipMalloc(&hist_, nh * 4));
+      HIPX(hipMalloc(&hoff_, nh * 4));
+      max_chunks_ = nbins_ + (max_entries_ + BIN_CHUNK - 1) / BIN_CHUNK;
+      const size_t nh2 = (max_chunks_ << fine_bits_) + 1;
+      HIPX(hipMalloc(&nch_, (nbins_ + 1) * 4));
+      HIPX(hipMalloc(&choff_, (nbins_ + 1) * 4));
+      HIPX(hipMalloc(&hist2_, nh2 * 4));
+      HIPX(hipMalloc(&hoff2_, nh2 * 4));
+    }
+  }
   HIPX(sort_pairs(nullptr, sort_tmp_bytes_, keys_, keys_sorted_, vals_, vals_sorted_, max_entries_, prm_.c - 1,
                   stream_));
   HIPX(hipMalloc(&sort_tmp_, std::max<size_t>(sort_tmp_bytes_, 4)));
-  HIPX(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_tmp_bytes_, cnt_, off_task_,
-                                        (int)std::max(nbuckets_ + 1, ncnt), stream_));
+  const size_t nscan = std::max(std::max(std::max(nbuckets_ + 1, ncnt), (size_t)nbins_ * grid_for(max_n_, TPB * BIN_R) + 1),
+                                (max_chunks_ << fine_bits_) + 1);
+  HIPX(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_tmp_bytes_, cnt_, off_task_, (int)nscan, stream_));
   HIPX(hipMalloc(&scan_tmp_, std::max<size_t>(scan_tmp_bytes_, 4)));
   HIPX(hipEventCreateWithFlags(&ready_, hipEventDisableTiming));
 }
@@ -293,7 +484,8 @@ MsmPlan::~MsmPlan() {
   if (ready_) (void)hipEventDestroy(ready_);
   if (h_valid_) (void)hipHostFree(h_valid_);
   for (void* p : {(void*)keys_, (void*)vals_, (void*)keys_sorted_, (void*)vals_sorted_, (void*)bstart_, (void*)bend_,
-                  (void*)cnt_, (void*)off_task_, sort_tmp_, scan_tmp_, (void*)bcnt_, (void*)boff_})
+                  (void*)cnt_, (void*)off_task_, sort_tmp_, scan_tmp_, (void*)bcnt_, (void*)boff_, (void*)hist_,
+                  (void*)hoff_, (void*)nch_, (void*)choff_, (void*)hist2_, (void*)hoff2_})
     if (p) (void)hipFree(p);
   for (auto* p : off_lvl_)
     if (p) (void)hipFree(p);
@@ -306,7 +498,39 @@ void MsmPlan::build(const uint32_t* scalars, size_t n) {
   const uint32_t nb = (uint32_t)nbuckets_;
   hipStream_t st = stream_;
   total_ = 0;
-  if (n > 0) {
+  if (use_bins_) {
+    // 1+2. bucket binning (k_bin_*, k_chunk_*): digits counted and scattered into coarse
+    //      bins, then each bin grouped by its fine key bits, bucket bounds on the way
+    HIPX(hipMemsetAsync(bstart_, 0, (nbuckets_ + 1) * 4, st));
+    HIPX(hipMemsetAsync(bend_, 0, (nbuckets_ + 1) * 4, st));
+    if (n > 0) {
+      const uint32_t nblk = grid_for(n, TPB * BIN_R);
+      const size_t nh = (size_t)nbins_ * nblk;
+      hipLaunchKernelGGL(k_bin_hist, dim3(nblk), dim3(TPB), 0, st, scalars, (uint32_t)n, prm_.c, (int)W, prm_.depth,
+                         fine_bits_, nbins_, hist_);
+      HIPX(hipMemsetAsync(hist_ + nh, 0, 4, st));
+      size_t stmp0 = scan_tmp_bytes_;
+      HIPX(hipcub::DeviceScan::ExclusiveSum(scan_tmp_, stmp0, hist_, hoff_, (int)(nh + 1), st));
+      hipLaunchKernelGGL(k_bin_scatter, dim3(nblk), dim3(TPB), 0, st, scalars, (uint32_t)n, prm_.c, (int)W,
+                         prm_.depth, fine_bits_, nbins_, hoff_, keys_, vals_);
+      hipLaunchKernelGGL(k_chunk_count, dim3(grid_for(nbins_ + 1)), dim3(TPB), 0, st, hoff_, nblk, nbins_, nch_);
+      size_t stmp1 = scan_tmp_bytes_;
+      HIPX(hipcub::DeviceScan::ExclusiveSum(scan_tmp_, stmp1, nch_, choff_, (int)(nbins_ + 1), st));
+      const size_t nh2 = (max_chunks_ << fine_bits_) + 1;  // unused tail stays zero
+      HIPX(hipMemsetAsync(hist2_, 0, nh2 * 4, st));
+      hipLaunchKernelGGL(k_chunk_hist, dim3((unsigned)max_chunks_), dim3(TPB), 0, st, keys_, hoff_, nblk, choff_,
+                         nbins_, fine_bits_, hist2_);
+      size_t stmp2 = scan_tmp_bytes_;
+      HIPX(hipcub::DeviceScan::ExclusiveSum(scan_tmp_, stmp2, hist2_, hoff2_, (int)nh2, st));
+      hipLaunchKernelGGL(k_chunk_scatter, dim3((unsigned)max_chunks_), dim3(TPB), 0, st, keys_, vals_, hoff_, nblk,
+                         choff_, nbins_, fine_bits_, hoff2_, vals_sorted_);
+      hipLaunchKernelGGL(k_chunk_bounds, dim3(grid_for(nbuckets_)), dim3(TPB), 0, st, choff_, fine_bits_, nb, hoff2_,
+                         bstart_, bend_);
+      HIPX(hipMemcpyAsync(h_valid_, hoff_ + nh, 4, hipMemcpyDeviceToHost, st));
+      HIPX(hipStreamSynchronize(st));
+      total_ = *h_valid_;
+    }
+  } else if (n > 0) {
     // 1. digits, compacted: only nonzero digits, window-major, point order within a window
     const uint32_t nblk = grid_for(n);
     hipLaunchKernelGGL(k_digit_count, dim3(nblk), dim3(TPB), 0, st, scalars, (uint32_t)n, prm_.c, (int)W, bcnt_);
@@ -319,9 +543,11 @@ void MsmPlan::build(const uint32_t* scalars, size_t n) {
     HIPX(hipStreamSynchronize(st));  // the sort needs the entry count on the host
     total_ = *h_valid_;
   }
-  HIPX(hipMemsetAsync(bstart_, 0, (nbuckets_ + 1) * 4, st));
-  HIPX(hipMemsetAsync(bend_, 0, (nbuckets_ + 1) * 4, st));
-  if (total_ > 0) {
+  if (!use_bins_) {
+    HIPX(hipMemsetAsync(bstart_, 0, (nbuckets_ + 1) * 4, st));
+    HIPX(hipMemsetAsync(bend_, 0, (nbuckets_ + 1) * 4, st));
+  }
+  if (!use_bins_ && total_ > 0) {
     // 2. stable LSD sort on the (c-1) bucket bits only: groups stay grouped (emission is
     //    window-major), so equal (group, bucket) keys end up contiguous
     size_t tmp = sort_tmp_bytes_;

@@ -116,8 +116,9 @@ class MsmPlan {
   MsmPlan(const MsmPlan&) = delete;
   MsmPlan& operator=(const MsmPlan&) = delete;
   // scalars: device, 8 LE 32-bit words each (standard form, any value < 2^256).
-  // Enqueues on the plan's stream and blocks the host once (the sort needs the
-  // number of nonzero digits); records ready() at the end.
+  // Enqueues on the plan's stream and blocks the host once (the task grid needs the
+  // number of nonzero digits); records ready() at the end.  Grouping by bucket: a stable
+  // rocprim radix sort, or with ZKP_PLAN_SORT=bins a two-level counting sort (msm.hip).
   void build(const uint32_t* scalars, size_t n);
   const MsmParams& params() const { return prm_; }
   hipEvent_t ready() const { return ready_; }
@@ -148,6 +149,13 @@ class MsmPlan {
   uint32_t *bstart_ = nullptr, *bend_ = nullptr, *cnt_ = nullptr, *off_task_ = nullptr;
   std::vector<uint32_t*> off_lvl_;
   uint32_t *bcnt_ = nullptr, *boff_ = nullptr;  // per (window, digit block) counts / offsets
+  // bucket binning (default grouping): coarse bins x binning blocks counts / offsets
+  bool use_bins_ = false;
+  int fine_bits_ = 0;
+  uint32_t nbins_ = 0;
+  uint32_t *hist_ = nullptr, *hoff_ = nullptr;
+  uint32_t *nch_ = nullptr, *choff_ = nullptr, *hist2_ = nullptr, *hoff2_ = nullptr;
+  size_t max_chunks_ = 0;
   uint32_t* h_valid_ = nullptr;                 // pinned: number of nonzero digits
   void* sort_tmp_ = nullptr;
   size_t sort_tmp_bytes_ = 0;
