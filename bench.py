@@ -113,38 +113,70 @@ def run_split(args, rank, world, local):
         from zkp_amd.dist import SplitProver
         sp = SplitProver(zk, local)
         sp.prover.stage(wit, slot=0)
+        distq = args.quotient == "dist"
+
+        def one():
+            if distq:
+                return sp.prove_raw_distq(wit, R_FIX, S_FIX, slot=0, staged=True)
+            return sp.prove_raw(wit, R_FIX, S_FIX, staged_slot=0)
         for _ in range(args.warmup):
-            sp.prove_raw(wit, R_FIX, S_FIX, staged_slot=0)
+            one()
         dist.barrier()
         torch.cuda.synchronize(local)
         t_start = time.perf_counter()
         for _ in range(args.steps):
-            res = sp.prove_raw(wit, R_FIX, S_FIX, staged_slot=0)
+            res = one()
         torch.cuda.synchronize(local)
         el = torch.tensor([time.perf_counter() - t_start], dtype=torch.float64, device="cuda:%d" % local)
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
         elapsed = float(el.item())
-        parts_desc = "%d ranks, RCCL all-gather of %d-byte partials" % (world, zkp_amd.PARTIAL_BYTES)
+        parts_desc = "%d ranks, RCCL all-gather of %d-byte partials, quotient %s" % (
+            world, zkp_amd.PARTIAL_BYTES,
+            "distributed (rank v%%G extends vector v, RCCL send/recv of domain slices)" if distq
+            else "recomputed on every rank")
         check = None
     else:
         nparts = args.parts
         provers = [zkp_amd.Prover(zk, devices=[local], part=k, nparts=nparts) for k in range(nparts)]
         for p in provers:
             p.stage(wit, slot=0)
+        distq = args.quotient == "dist"
+        n = provers[0].domain_size
+        full = [torch.empty(n * 32, dtype=torch.uint8, device="cuda:%d" % local) for _ in range(3)] if distq else None
+
+        def one(per):
+            parts = []
+            if distq:  # rank k's work = its quotient vectors + its slice; the exchange is a device copy here
+                for k, p in enumerate(provers):
+                    mine = [v for v in range(3) if v % nparts == k]
+                    t1 = time.perf_counter()
+                    if mine:
+                        p.quotient_part_staged(0, sum(1 << v for v in mine),
+                                               [full[v].data_ptr() if v in mine else None for v in range(3)])
+                    per[k] += time.perf_counter() - t1
+                for k, p in enumerate(provers):
+                    lo, hi = n * k // nparts, n * (k + 1) // nparts
+                    sl = [full[v][lo * 32:hi * 32].clone() for v in range(3)]
+                    torch.cuda.synchronize(local)
+                    t1 = time.perf_counter()
+                    parts.append(p.prove_partial_ext_staged(0, [t.data_ptr() for t in sl]))
+                    per[k] += time.perf_counter() - t1
+            else:
+                for k, p in enumerate(provers):
+                    t1 = time.perf_counter()
+                    parts.append(p.prove_partial_staged(0))
+                    per[k] += time.perf_counter() - t1
+            return parts
         for _ in range(args.warmup):
-            [p.prove_partial_staged(0) for p in provers]
+            one([0.0] * nparts)
         per = [0.0] * nparts
         t_start = time.perf_counter()
         for _ in range(args.steps):
-            parts = []
-            for k, p in enumerate(provers):
-                t1 = time.perf_counter()
-                parts.append(p.prove_partial_staged(0))
-                per[k] += time.perf_counter() - t1
-            res = zkp_amd.proof_combine_raw(zk, parts, wit, R_FIX, S_FIX)
+            res = zkp_amd.proof_combine_raw(zk, one(per), wit, R_FIX, S_FIX)
         elapsed = time.perf_counter() - t_start
-        parts_desc = "%d slices emulated one after another on 1 GPU; per-slice ms %s" % (
-            nparts, [round(x / args.steps * 1e3, 2) for x in per])
+        parts_desc = "%d slices emulated one after another on 1 GPU, quotient %s; per-slice ms %s" % (
+            nparts, "distributed" if distq else "recomputed per slice",
+            [round(x / args.steps * 1e3, 2) for x in per])
         del provers
         full = zkp_amd.Prover(zk, devices=[local])
         check = full.prove_raw(wit, R_FIX, S_FIX) == res
@@ -174,6 +206,8 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-kernels", action="store_true")
     ap.add_argument("--scale", type=float, default=1.0, help="fraction of the Venmo shape (smoke/debug only)")
+    ap.add_argument("--quotient", choices=["dist", "full"], default="dist",
+                    help="split mode: distribute the three coset extensions over the ranks, or recompute per rank")
     ap.add_argument("--mode", choices=["replicas", "split"], default="replicas",
                     help="replicas: independent proofs per GPU (headline); split: configs[4], one proof over GPUs")
     ap.add_argument("--parts", type=int, default=2, help="split mode in one process: slices on one GPU")

@@ -176,6 +176,18 @@ zkp_status zkp_witness_stage(zkp_prover* p, int dev_index, int slot, const uint8
 zkp_status zkp_prove_staged(zkp_prover* p, int dev_index, int slot, const uint8_t* r32, const uint8_t* s32,
                             zkp_proof* out);
 zkp_status zkp_prove_partial_staged(zkp_prover* p, int slot, zkp_partial* out);
+/* Distributed quotient of a split proof: instead of every part
+ * recomputing all three coset extensions, part v % nparts computes vector v (A, B, C) and
+ * the parts exchange domain slices (zkp_amd.dist: RCCL send/recv over xGMI).
+ * Stage 1: buildABC on the witness staged in `slot`, then the coset extension of the
+ * vectors selected by mask (bit 0 A, 1 B, 2 C); vector v is copied whole (domain_size x
+ * 32 bytes, opaque device layout) to dst[v], device memory on this prover's device
+ * (entries of unselected vectors may be NULL).  Returns when the copies are complete. */
+zkp_status zkp_quotient_part_staged(zkp_prover* p, int slot, int mask, void* const* dst);
+/* Stage 2: the partial sums of this prover's slice with the H-MSM scalars joined from
+ * abc[0..2] = device pointers to the stage-1 values of A, B, C at this part's domain
+ * slice [part*n/nparts, (part+1)*n/nparts) (contiguous, complete before the call). */
+zkp_status zkp_prove_partial_ext_staged(zkp_prover* p, int slot, const void* const* abc, zkp_partial* out);
 /* Bracket every bucket-accumulate kernel launch with HIP events (on its stream).
  * zkp_prover_kernel_stats: [0] G1 accumulate ms (sum), [1] G1 launches, [2] G1 mixed
  * additions, [3] G1 tasks, [4..7] the same for G2.  Enabling resets the counters. */

@@ -32,3 +32,33 @@ def test_full_prover_partial_is_part_0_of_1():
     (a, b, c), _ = zkp_amd.proof_combine_raw(zk, [part], wt, r, s)
     assert {"A": a, "B": b, "C": c} == want
     assert p.prove_raw(wt, r, s)[0] == (a, b, c)
+
+
+@pytest.mark.parametrize("name,nparts", [("small", 2), ("small", 3), ("venmo_mini", 4)])
+def test_split_distributed_quotient(name, nparts):
+    # the distributed quotient on one GPU: part v % nparts extends vector v only
+    # (zkp_quotient_part_staged), every part joins just its domain slice from the exchanged
+    # slices (zkp_prove_partial_ext_staged); partials and proof stay bit-exact
+    import torch
+    from zkp_amd.dist import split_range
+    zk, wt, r, s, want = _case(name)
+    provers = [zkp_amd.Prover(zk, devices=[0], part=k, nparts=nparts) for k in range(nparts)]
+    n = provers[0].domain_size
+    full = [torch.empty(n * 32, dtype=torch.uint8, device="cuda") for _ in range(3)]
+    for k, p in enumerate(provers):
+        p.stage(wt, 0)
+        mine = [v for v in range(3) if v % nparts == k]
+        if mine:
+            p.quotient_part_staged(0, sum(1 << v for v in mine),
+                                   [full[v].data_ptr() if v in mine else None for v in range(3)])
+    parts = []
+    for k, p in enumerate(provers):
+        lo, hi = split_range(n, k, nparts)
+        sl = [full[v][lo * 32:hi * 32].clone() for v in range(3)]
+        torch.cuda.synchronize()
+        parts.append(p.prove_partial_ext_staged(0, [t.data_ptr() for t in sl]))
+    for p in provers:
+        p.close()
+    assert parts == _oracle_partials(zk, wt, nparts)
+    (a, b, c), _ = zkp_amd.proof_combine_raw(zk, parts, wt, r, s)
+    assert {"A": a, "B": b, "C": c} == want

@@ -95,3 +95,41 @@ def test_split_allgather_gloo_world2():
     for rank, tags, (a, b, c) in res:
         assert tags == [k.to_bytes(4, "little") + (2).to_bytes(4, "little") for k in range(2)]  # rank order
         assert {"A": a, "B": b, "C": c} == want
+
+
+def _xchg_worker(rank, world, port, n, q):
+    import torch
+    import torch.distributed as dist
+    from zkp_amd.dist import exchange_quotient_slices, split_range
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        def vec(v):  # deterministic stand-in for the coset evaluations of A, B, C
+            g = torch.Generator().manual_seed(100 + v)
+            return torch.randint(0, 256, (n * 32,), dtype=torch.uint8, generator=g)
+        full = [vec(v) if v % world == rank else None for v in range(3)]
+        got = exchange_quotient_slices(full, n, 32, None, torch.device("cpu"))
+        lo, hi = split_range(n, rank, world)
+        ok = all(torch.equal(got[v], vec(v)[lo * 32:hi * 32]) for v in range(3))
+        q.put((rank, ok))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n", [(2, 64), (3, 50), (4, 37)])
+def test_distributed_quotient_exchange_gloo(world, n):
+    # the slice exchange of the distributed quotient (zkp_amd.dist.exchange_quotient_slices,
+    # RCCL point-to-point on GPUs): rank v % world owns vector v, every rank ends up with its
+    # domain slice of all three, ragged slice sizes included
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_xchg_worker, args=(k, world, port, n, q)) for k in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    assert res == {k: True for k in range(world)}

@@ -227,6 +227,16 @@ zkp_status zkp_prove_partial_staged(zkp_prover* p, int slot, zkp_partial* out) {
   return guard([&] { p->impl->prove_partial_staged(slot, out); });
 }
 
+zkp_status zkp_quotient_part_staged(zkp_prover* p, int slot, int mask, void* const* dst) {
+  if (!p || !dst) return fail(ZKP_ERR_INVALID_ARG, "null argument");
+  return guard([&] { p->impl->quotient_part_staged(slot, mask, dst); });
+}
+
+zkp_status zkp_prove_partial_ext_staged(zkp_prover* p, int slot, const void* const* abc, zkp_partial* out) {
+  if (!p || !abc || !out) return fail(ZKP_ERR_INVALID_ARG, "null argument");
+  return guard([&] { p->impl->prove_partial_ext_staged(slot, abc, out); });
+}
+
 zkp_status zkp_proof_combine(const uint8_t* zkey, size_t len, const zkp_partial* parts, int nparts,
                              const uint8_t* wtns, size_t wlen, const uint8_t* r32, const uint8_t* s32,
                              zkp_proof* out) {

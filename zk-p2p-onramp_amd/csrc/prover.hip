@@ -501,6 +501,47 @@ class DevicePipeline {
     float ms[6];
   };
 
+  // Distributed quotient of a split proof, stage 1: buildABC on the
+  // witness in `slot`, then the coset extension (rows A5-A7) of the vectors in mask (bit 0
+  // A, 1 B, 2 C) only, each copied whole (domain x 32 bytes, device layout: Montgomery
+  // 2^261, 8 packed words) to dst[v], device memory on this device.  Returns when done.
+  void quotient_part_staged(int slot, int mask, void* const* dst) {
+    std::lock_guard<std::mutex> lk(mu_);
+    HIPX(hipSetDevice(dev_));
+    const uint32_t* d = slot_ptr(slot);
+    const ZkeyHeader& h = hdr_;
+    launch_build_abc(rowptr_[0], col_[0], val_[0], rowptr_[1], col_[1], val_[1], d, h.domain_size, abc_[0], abc_[1],
+                     abc_[2], s0_);
+    for (int v = 0; v < 3; ++v) {
+      if (!(mask >> v & 1)) continue;
+      if (!dst[v]) throw ZkpError(ZKP_ERR_INVALID_ARG, "quotient part: null destination");
+      ntt_->coset_extend(abc_[v]);
+      HIPX(hipMemcpyAsync(dst[v], abc_[v], (size_t)h.domain_size * 32, hipMemcpyDeviceToDevice, s0_));
+    }
+    HIPX(hipStreamSynchronize(s0_));
+  }
+
+  // stage 2: this slice's partial sums with the H scalars joined (row A8) from abc[0..2] =
+  // the coset evaluations of A, B, C at this part's domain slice (device memory, ready)
+  MsmOut prove_ext_staged(int slot, const void* const* abc) {
+    std::lock_guard<std::mutex> lk(mu_);
+    HIPX(hipSetDevice(dev_));
+    const uint32_t* d = slot_ptr(slot);
+    for (int v = 0; v < 3; ++v)
+      if (!abc[v]) throw ZkpError(ZKP_ERR_INVALID_ARG, "partial prove: null quotient slice");
+    HIPX(hipEventRecord(ev_[0], s0_));
+    HIPX(hipEventRecord(ev_[1], s0_));
+    for (int v = 0; v < 3; ++v) ext_abc_[v] = static_cast<const uint32_t*>(abc[v]);
+    try {
+      MsmOut o = prove_dev(d);
+      for (auto& e : ext_abc_) e = nullptr;
+      return o;
+    } catch (...) {
+      for (auto& e : ext_abc_) e = nullptr;
+      throw;
+    }
+  }
+
   MsmOut prove(const WtnsView& w) {
     std::lock_guard<std::mutex> lk(mu_);
     HIPX(hipSetDevice(dev_));
@@ -602,7 +643,13 @@ class DevicePipeline {
     auto h_job = [&] {
       try {
         if (serial_) HIPX(hipStreamWaitEvent(s0_, ev_[6], 0));
-        enqueue_quotient(d_wit);
+        if (ext_abc_[0]) {  // distributed quotient: only the join of this domain slice
+          HIPX(hipEventRecord(ev_[2], s0_));
+          launch_join_abc(ext_abc_[0], ext_abc_[1], ext_abc_[2], (uint32_t)(hhi_ - hlo_), pscal_ + hlo_ * 8, s0_);
+          HIPX(hipEventRecord(ev_[3], s0_));
+        } else {
+          enqueue_quotient(d_wit);
+        }
         qdone.set_value();
         qdone_set = true;
         if (s4_) HIPX(hipStreamWaitEvent(s4_, ev_[3], 0));
@@ -674,6 +721,7 @@ class DevicePipeline {
   uint32_t* wit_ = nullptr;
   uint32_t* abc_[3] = {nullptr, nullptr, nullptr};
   uint32_t* pscal_ = nullptr;
+  const uint32_t* ext_abc_[3] = {nullptr, nullptr, nullptr};  // set only inside prove_ext_staged
   std::unique_ptr<NttEngine> ntt_;
   std::unique_ptr<MsmPlan> plan_w_, plan_h_;
   std::unique_ptr<MsmEngine> g1w_[3], g1h_, g2_;  // g1w_: A, B1, C
@@ -804,6 +852,19 @@ void Prover::prove_partial(const uint8_t* wtns, size_t len, zkp_partial* out) {
 
 void Prover::prove_partial_staged(int slot, zkp_partial* out) {
   DevicePipeline::MsmOut m = devs_[0]->prove_staged(slot);
+  msm_out_to_partial(m, part_, nparts_, out);
+  std::lock_guard<std::mutex> lk(tmu_);
+  for (int i = 0; i < 5; ++i) last_ms_[i] = m.ms[i];
+  last_ms_[7] = m.ms[5];
+}
+
+void Prover::quotient_part_staged(int slot, int mask, void* const* dst) {
+  if (mask < 0 || mask > 7) throw ZkpError(ZKP_ERR_INVALID_ARG, "quotient part: mask must be within 0..7");
+  devs_[0]->quotient_part_staged(slot, mask, dst);
+}
+
+void Prover::prove_partial_ext_staged(int slot, const void* const* abc, zkp_partial* out) {
+  DevicePipeline::MsmOut m = devs_[0]->prove_ext_staged(slot, abc);
   msm_out_to_partial(m, part_, nparts_, out);
   std::lock_guard<std::mutex> lk(tmu_);
   for (int i = 0; i < 5; ++i) last_ms_[i] = m.ms[i];

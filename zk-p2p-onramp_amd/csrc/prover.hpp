@@ -82,6 +82,9 @@ class Prover {
   // point-range split of one proof: this slice's MSM partial sums
   void prove_partial(const uint8_t* wtns, size_t len, zkp_partial* out);
   void prove_partial_staged(int slot, zkp_partial* out);
+  // distributed quotient of a split proof (zkp_quotient_part_staged / zkp_prove_partial_ext_staged)
+  void quotient_part_staged(int slot, int mask, void* const* dst);
+  void prove_partial_ext_staged(int slot, const void* const* abc, zkp_partial* out);
   int part() const { return part_; }
   int nparts() const { return nparts_; }
   // MSM configuration of device 0: [0] witness c, [1] witness depth, [2] witness groups,

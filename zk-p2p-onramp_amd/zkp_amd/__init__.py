@@ -116,13 +116,16 @@ def load_library(path: str = LIB_PATH):
         lib.zkp_prove_partial_staged.argtypes = [P, ctypes.c_int, ctypes.c_char_p]
         lib.zkp_proof_combine.argtypes = [u8p, sz, ctypes.c_char_p, ctypes.c_int, u8p, sz, u8p, u8p,
                                           ctypes.POINTER(_Proof)]
+        lib.zkp_quotient_part_staged.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.POINTER(P)]
+        lib.zkp_prove_partial_ext_staged.argtypes = [P, ctypes.c_int, ctypes.POINTER(P), ctypes.c_char_p]
         for name in ("zkp_prover_load_mem", "zkp_prover_load_file", "zkp_prover_info", "zkp_prove",
                      "zkp_prove_batch", "zkp_prove_files", "zkp_proof_json", "zkp_public_json",
                      "zkp_prover_timings", "zkp_msm_g1", "zkp_msm_g2", "zkp_ntt_fr", "zkp_quotient",
                      "zkp_witness_stage", "zkp_prove_staged", "zkp_prover_instrument", "zkp_prover_kernel_stats",
                      "zkp_bench_msm", "zkp_bench_ntt", "zkp_msm", "zkp_prover_msm_config",
                      "zkp_prover_load_part", "zkp_prove_partial", "zkp_proof_calldata",
-                     "zkp_prover_load_chunks", "zkp_zkey_read", "zkp_zkey_read_chunks", "zkp_zkey_contribute", "zkp_prove_partial_staged", "zkp_proof_combine"):
+                     "zkp_prover_load_chunks", "zkp_zkey_read", "zkp_zkey_read_chunks", "zkp_zkey_contribute", "zkp_prove_partial_staged", "zkp_proof_combine",
+                     "zkp_quotient_part_staged", "zkp_prove_partial_ext_staged"):
             getattr(lib, name).restype = ctypes.c_int
         _lib = lib
         return lib
@@ -310,6 +313,22 @@ class Prover:
     def prove_partial_staged(self, slot: int) -> bytes:
         out = ctypes.create_string_buffer(PARTIAL_BYTES)
         _check(load_library().zkp_prove_partial_staged(self._h, slot, out))
+        return out.raw
+
+    def quotient_part_staged(self, slot: int, mask: int, dst_ptrs):
+        """Distributed quotient, stage 1 (zkp_quotient_part_staged): coset extensions of the
+        vectors in mask (bit 0 A, 1 B, 2 C) of the witness staged in `slot`, each copied to
+        the device pointer dst_ptrs[v] (domain_size x 32 bytes; None for unselected)."""
+        arr = (ctypes.c_void_p * 3)(*[p or None for p in dst_ptrs])
+        _check(load_library().zkp_quotient_part_staged(self._h, slot, mask, arr))
+
+    def prove_partial_ext_staged(self, slot: int, abc_ptrs) -> bytes:
+        """Distributed quotient, stage 2 (zkp_prove_partial_ext_staged): this slice's
+        partial sums with the H scalars joined from device pointers abc_ptrs[0..2] (A, B, C
+        at this part's domain slice)."""
+        arr = (ctypes.c_void_p * 3)(*abc_ptrs)
+        out = ctypes.create_string_buffer(PARTIAL_BYTES)
+        _check(load_library().zkp_prove_partial_ext_staged(self._h, slot, arr, out))
         return out.raw
 
     def msm_config(self):

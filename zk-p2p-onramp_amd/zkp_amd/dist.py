@@ -8,7 +8,11 @@ on ROCm, "gloo" for CPU tests).  Two scaling modes:
   computes its MSM partial sums (zkp_prove_partial, 392 bytes), and ONE all-gather of
   G x 392 bytes over xGMI brings every slice's partials to every rank, which sums them
   and assembles the proof on the host (zkp_proof_combine) -- bit-identical to the
-  single-GPU proof.  The quotient H is computed in full by every rank.
+  single-GPU proof.  The quotient: either every rank computes it in full
+  (SplitProver.prove_raw), or it is distributed (SplitProver.prove_raw_distq, SURVEY
+  §8e E1(2)): rank v % G computes the coset extension of vector v in {A, B, C} and sends
+  every rank the domain slice it needs (RCCL point-to-point over xGMI), so each rank only
+  joins its own slice.
 """
 from __future__ import annotations
 
@@ -16,6 +20,41 @@ import torch
 import torch.distributed as dist
 
 from . import PARTIAL_BYTES, Prover, proof_combine_raw
+
+
+def split_range(n: int, part: int, nparts: int):
+    """[lo, hi) of slice `part` of n items cut into nparts contiguous ranges (as the C++
+    split_range in prover.hip)."""
+    return n * part // nparts, n * (part + 1) // nparts
+
+
+def exchange_quotient_slices(full, n: int, elem_bytes: int, group=None, device=None):
+    """Redistribute the three quotient vectors A, B, C (n elements of elem_bytes each):
+    rank v % G holds full[v] (a uint8 tensor of n * elem_bytes bytes; other entries are
+    ignored); every rank receives its slice split_range(n, rank, G) of each vector.
+    Owners send with batched point-to-point operations (no collective over the whole
+    vector).  Returns [slice_A, slice_B, slice_C] as uint8 tensors on `device`."""
+    rank = dist.get_rank(group)
+    world = dist.get_world_size(group)
+    lo, hi = split_range(n, rank, world)
+    out = [torch.empty((hi - lo) * elem_bytes, dtype=torch.uint8, device=device) for _ in range(3)]
+    ops = []
+    for v in range(3):
+        owner = v % world
+        if rank == owner:
+            for k in range(world):
+                klo, khi = split_range(n, k, world)
+                sl = full[v][klo * elem_bytes:khi * elem_bytes]
+                if k == rank:
+                    out[v].copy_(sl)
+                elif khi > klo:
+                    ops.append(dist.P2POp(dist.isend, sl, dist.get_global_rank(group, k) if group else k, group))
+        elif hi > lo:
+            ops.append(dist.P2POp(dist.irecv, out[v], dist.get_global_rank(group, owner) if group else owner, group))
+    if ops:
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
+    return out
 
 
 def _gather_device(group):
@@ -57,5 +96,23 @@ class SplitProver:
         equal on all ranks (None draws them per rank: pass explicit values in production
         so that every rank assembles the same proof, or use rank 0's result)."""
         part = self.prover.prove_partial_staged(staged_slot) if staged_slot is not None else self.partial(wtns)
+        parts = all_gather_partials(part, self.group)
+        return proof_combine_raw(self.zkey, parts, wtns, r, s)
+
+    def prove_raw_distq(self, wtns: bytes, r=None, s=None, slot: int = 0, staged: bool = False):
+        """As prove_raw, with the quotient distributed over the ranks (needs the "nccl"
+        backend: the slices move between GPUs).  staged=True: the witness is already in
+        `slot` (Prover.stage)."""
+        if not staged:
+            self.prover.stage(wtns, slot)
+        n = self.prover.domain_size
+        dev = torch.device("cuda", torch.cuda.current_device())
+        mine = [v for v in range(3) if v % self.world == self.rank]
+        full = [torch.empty(n * 32, dtype=torch.uint8, device=dev) if v in mine else None for v in range(3)]
+        self.prover.quotient_part_staged(slot, sum(1 << v for v in mine),
+                                         [t.data_ptr() if t is not None else None for t in full])
+        sl = exchange_quotient_slices(full, n, 32, self.group, dev)
+        torch.cuda.synchronize()
+        part = self.prover.prove_partial_ext_staged(slot, [t.data_ptr() for t in sl])
         parts = all_gather_partials(part, self.group)
         return proof_combine_raw(self.zkey, parts, wtns, r, s)
