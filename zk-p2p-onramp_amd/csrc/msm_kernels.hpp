@@ -114,7 +114,14 @@ ZDEV void accumulate(uint32_t t, const uint32_t* __restrict__ points, const uint
   const uint32_t s0 = start[b] + (t - off[b]) * S;
   const uint32_t s1 = umin(end[b], s0 + S);
   Xyzz<F> acc = xyzz_inf<F>();
-  for (uint32_t j = s0; j < s1; ++j) {
+  uint32_t j = s0;
+  if (s1 - s0 >= 2) {  // the first two entries as an affine + affine addition
+    const uint32_t v0 = vals[s0], v1 = vals[s0 + 1];
+    acc = xyzz_from_aff_pair(load_aff<F>(points, v0 & 0x7fffffffu), (v0 >> 31) != 0,
+                             load_aff<F>(points, v1 & 0x7fffffffu), (v1 >> 31) != 0);
+    j = s0 + 2;
+  }
+  for (; j < s1; ++j) {
     const uint32_t v = vals[j];
     xyzz_add_aff(acc, load_aff<F>(points, v & 0x7fffffffu), (v >> 31) != 0);
   }
