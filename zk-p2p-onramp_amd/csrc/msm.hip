@@ -90,6 +90,25 @@ __global__ __launch_bounds__(TPB) void k_digit_write(const uint32_t* __restrict_
   }
 }
 
+// dense emission (uniform scalars: nearly every digit is nonzero): entry w*n + i for every
+// (window, point), a zero digit keyed `sentinel` (= the bucket count, sorted past every
+// bucket) -- no counting pass, no scan, no host round trip for the entry count
+__global__ __launch_bounds__(TPB) void k_digit_write_dense(const uint32_t* __restrict__ scalars, uint32_t n, int c,
+                                                           int W, int T, uint32_t sentinel,
+                                                           uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+  const uint32_t i = blockIdx.x * TPB + threadIdx.x;
+  if (i >= n) return;
+  uint32_t s[9];
+  msmk::load_scalar(scalars, i, s);
+  uint32_t carry = 0;
+  for (int w = 0; w < W; ++w) {
+    uint32_t key, val;
+    const bool valid = msmk::digit_entry(s, w, c, T, n, i, carry, key, val);
+    keys[(size_t)w * n + i] = valid ? key : sentinel;
+    vals[(size_t)w * n + i] = val;
+  }
+}
+
 __global__ __launch_bounds__(TPB) void k_bounds(const uint32_t* __restrict__ keys, uint32_t total,
                                                 uint32_t* __restrict__ start, uint32_t* __restrict__ end) {
   msmk::bounds(blockIdx.x * TPB + threadIdx.x, keys, total, start, end);
@@ -472,6 +491,12 @@ MsmPlan::MsmPlan(size_t max_n, const MsmParams& prm, hipStream_t stream)
   }
   HIPX(sort_pairs(nullptr, sort_tmp_bytes_, keys_, keys_sorted_, vals_, vals_sorted_, max_entries_, prm_.c - 1,
                   stream_));
+  while ((size_t(1) << dense_bits_) <= nbuckets_) ++dense_bits_;
+  {
+    size_t dense_tmp = 0;
+    HIPX(sort_pairs(nullptr, dense_tmp, keys_, keys_sorted_, vals_, vals_sorted_, max_entries_, dense_bits_, stream_));
+    sort_tmp_bytes_ = std::max(sort_tmp_bytes_, dense_tmp);
+  }
   HIPX(hipMalloc(&sort_tmp_, std::max<size_t>(sort_tmp_bytes_, 4)));
   const size_t nscan = std::max(std::max(std::max(nbuckets_ + 1, ncnt), (size_t)nbins_ * grid_for(max_n_, TPB * BIN_R) + 1),
                                 (max_chunks_ << fine_bits_) + 1);
@@ -498,7 +523,19 @@ void MsmPlan::build(const uint32_t* scalars, size_t n) {
   const uint32_t nb = (uint32_t)nbuckets_;
   hipStream_t st = stream_;
   total_ = 0;
-  if (use_bins_) {
+  if (dense_ && !use_bins_) {
+    // 1+2. dense digits (no compaction) and a full sort on the key bits + sentinel bit
+    HIPX(hipMemsetAsync(bstart_, 0, (nbuckets_ + 1) * 4, st));
+    HIPX(hipMemsetAsync(bend_, 0, (nbuckets_ + 1) * 4, st));
+    total_ = (uint32_t)(n * W);
+    if (total_ > 0) {
+      hipLaunchKernelGGL(k_digit_write_dense, dim3(grid_for(n)), dim3(TPB), 0, st, scalars, (uint32_t)n, prm_.c,
+                         (int)W, prm_.depth, nb, keys_, vals_);
+      size_t tmp = sort_tmp_bytes_;
+      HIPX(sort_pairs(sort_tmp_, tmp, keys_, keys_sorted_, vals_, vals_sorted_, (size_t)total_, dense_bits_, st));
+      hipLaunchKernelGGL(k_bounds, dim3(grid_for(total_)), dim3(TPB), 0, st, keys_sorted_, total_, bstart_, bend_);
+    }
+  } else if (use_bins_) {
     // 1+2. bucket binning (k_bin_*, k_chunk_*): digits counted and scattered into coarse
     //      bins, then each bin grouped by its fine key bits, bucket bounds on the way
     HIPX(hipMemsetAsync(bstart_, 0, (nbuckets_ + 1) * 4, st));
@@ -543,11 +580,12 @@ void MsmPlan::build(const uint32_t* scalars, size_t n) {
     HIPX(hipStreamSynchronize(st));  // the sort needs the entry count on the host
     total_ = *h_valid_;
   }
-  if (!use_bins_) {
+  const bool compacted = !use_bins_ && !dense_;
+  if (compacted) {
     HIPX(hipMemsetAsync(bstart_, 0, (nbuckets_ + 1) * 4, st));
     HIPX(hipMemsetAsync(bend_, 0, (nbuckets_ + 1) * 4, st));
   }
-  if (!use_bins_ && total_ > 0) {
+  if (compacted && total_ > 0) {
     // 2. stable LSD sort on the (c-1) bucket bits only: groups stay grouped (emission is
     //    window-major), so equal (group, bucket) keys end up contiguous
     size_t tmp = sort_tmp_bytes_;

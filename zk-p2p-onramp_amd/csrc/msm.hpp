@@ -120,6 +120,11 @@ class MsmPlan {
   // number of nonzero digits); records ready() at the end.  Grouping by bucket: a stable
   // rocprim radix sort, or with ZKP_PLAN_SORT=bins a two-level counting sort (msm.hip).
   void build(const uint32_t* scalars, size_t n);
+  // dense emission (for uniform scalars, e.g. the H MSM's): every (window, point) digit is an
+  // entry, zero digits keyed past the last bucket, so build() never blocks the host and the
+  // entry count is the bound n * W (entries() then counts the rare zero digits too)
+  void set_dense(bool d) { dense_ = d; }
+  bool dense() const { return dense_; }
   const MsmParams& params() const { return prm_; }
   hipEvent_t ready() const { return ready_; }
   hipStream_t stream() const { return stream_; }
@@ -151,6 +156,8 @@ class MsmPlan {
   uint32_t *bcnt_ = nullptr, *boff_ = nullptr;  // per (window, digit block) counts / offsets
   // bucket binning (default grouping): coarse bins x binning blocks counts / offsets
   bool use_bins_ = false;
+  bool dense_ = false;
+  int dense_bits_ = 0;                          // key bits of the dense sort (sentinel = buckets)
   int fine_bits_ = 0;
   uint32_t nbins_ = 0;
   uint32_t *hist_ = nullptr, *hoff_ = nullptr;

@@ -392,6 +392,9 @@ class DevicePipeline {
     // quotient on s0, which then plans and runs the H MSM
     plan_w_ = std::make_unique<MsmPlan>(nv, pw, s2_);
     plan_h_ = std::make_unique<MsmPlan>(nd, ph, s4_ ? s4_ : s0_);
+    // H scalars are uniform (quotient evaluations): dense digits, so the H plan never blocks
+    // its host thread and the chain quotient -> plan -> H MSM is enqueued in one go
+    plan_h_->set_dense(env_int("ZKP_H_DENSE", 1) != 0);
     for (auto& g : g1w_) g = std::make_unique<MsmEngine>(Curve::G1, pw, nv, s2_);
     g2_ = std::make_unique<MsmEngine>(Curve::G2, pw, nv, s1_);
     g1h_ = std::make_unique<MsmEngine>(Curve::G1, ph, nd, s0_);
