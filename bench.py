@@ -82,13 +82,31 @@ def kernel_benches(device, log_n=20, iters=10):
     scal = synth.scalars(CIRCUIT_SEED, 1, n)
     st, res = zkp_amd.bench_msm(pts, scal, g2=False, warmup=2, iters=iters, device=device)
     ntt_ms = zkp_amd.bench_ntt(log_n, warmup=2, iters=iters, device=device)
+    ntt23_ms = zkp_amd.bench_ntt(23, warmup=2, iters=iters, device=device)
     return {
         "msm_g1_2^20_ms": round(st["ms_per_msm"], 3),
         "msm_g1_2^20_Mpts_per_s": round(n / st["ms_per_msm"] / 1e3, 1),
         "msm_g1_2^20_accumulate_ms": round(st["ms_accumulate"], 3),
         "msm_window_bits": st["c"],
         "ntt_fr_2^20_coset_extend_ms": round(ntt_ms, 3),
+        "ntt_roofline": {"2^20": ntt_roofline(log_n, ntt_ms), "2^23 (Venmo domain)": ntt_roofline(23, ntt23_ms)},
     }, st
+
+
+def ntt_roofline(log_n, ms):
+    """Roofline of one coset extension (iNTT -> coset key g^i/n -> NTT) of 2^log_n
+    Fr elements.  Algorithmic work: 2 * (n/2) * log2 n butterfly products + n key products, 136 MAC per Fr
+    mul; algorithmic bytes: one read + one write of n x 32 B.  Four-step passes of <= 8
+    bits: 2 * ceil(log_n / 8) - 1 HBM round trips (the innermost inverse/forward pair is fused)."""
+    n = 1 << log_n
+    peak, _ = load_peak()
+    mac = (2 * (n // 2) * log_n + n) * MAC_PER_FPMUL
+    achieved = mac / (ms * 1e-3) / 1e12
+    passes = 2 * ((log_n + 7) // 8) - 1
+    return {"bound": "valu-int", "ms": round(ms, 4), "achieved": round(achieved, 3), "peak": peak,
+            "unit": "TMAC/s", "frac": round(achieved / peak, 4) if peak else None,
+            "hbm_pass_GBps": round(passes * 64 * n / (ms * 1e-3) / 1e9, 1),
+            "hbm_frac_of_8TBps": round(passes * 64 * n / (ms * 1e-3) / 8e12, 4)}
 
 
 S24 = dict(n_vars=16_000_000, n_constraints=(1 << 24) - 27, n_public=26)  # configs[4] (SURVEY.md §8d D2)
@@ -345,8 +363,15 @@ def main():
     }
 
     if not args.no_kernels:
-        kb, _ = kernel_benches(local)
+        kb, kst = kernel_benches(local)
         out["kernels_config1"] = kb
+        if peak and kst["ms_accumulate"] > 0:
+            # the same kernel alone on the GPU (configs[1] G1 MSM 2^20, uniform scalars): the in-proof
+            # average above is stretched by the three other streams sharing the CUs
+            iso = kst["mixed_adds"] * FPMUL_PER_MADD * MAC_PER_FPMUL / (kst["ms_accumulate"] * 1e-3) / 1e12
+            roofline["isolated_launch"] = {"workload": "configs[1] G1 MSM 2^20 accumulate, kernel alone",
+                                           "mixed_adds": kst["mixed_adds"], "avg_launch_ms": round(kst["ms_accumulate"], 4),
+                                           "achieved": round(iso, 3), "frac": round(iso / peak, 4)}
 
     if args.cpu_baseline == "full":
         try:

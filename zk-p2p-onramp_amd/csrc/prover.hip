@@ -583,6 +583,8 @@ class DevicePipeline {
     // quotient, so the quotient -> H plan -> H MSM chain gets the GPU first.  Measured: no
     // gain (33.7 vs 33.5 ms): the proof is bound by the total work, not by the chain, so
     // the default lets every stream run freely.  Never in the serial profiling mode.
+    // Modes 4 / 5 gate only the G2 MSM (on the quotient / on the H plan too), so its long
+    // accumulation fills the H-plan window instead of competing with the quotient.
     const bool gate = !serial_ && sched_gate_;
     std::promise<void> qdone;
     std::shared_future<void> qdone_f = qdone.get_future().share();
@@ -598,7 +600,7 @@ class DevicePipeline {
         plan_w_->build(d_wit + wlo_ * 8, whi_ - wlo_);
         planned.set_value();
         planned_set = true;
-        if (gate) {  // accumulate only once the quotient (head of the critical H chain) is done
+        if (gate && gate_mode_ < 4) {  // accumulate only once the quotient (head of the critical H chain) is done
           qdone_f.get();
           HIPX(hipStreamWaitEvent(s2_, ev_[3], 0));
           if (gate_mode_ >= 2) {  // ... and the H plan
@@ -631,7 +633,7 @@ class DevicePipeline {
         if (gate && gate_mode_ != 3) {  // mode 3: the G2 MSM (longest finish) runs from the start
           qdone_f.get();
           HIPX(hipStreamWaitEvent(s1_, ev_[3], 0));
-          if (gate_mode_ == 2) {
+          if (gate_mode_ == 2 || gate_mode_ == 5) {
             hdone_f.get();
             HIPX(hipStreamWaitEvent(s1_, plan_h_->ready(), 0));
           }
