@@ -69,6 +69,15 @@ def main(n=300):
             checks.append(("mulf2", lambda v, x=e[k]: v % P == x * inv_rp_p % P and v < 2 * P))
         for k in range(2):
             checks.append(("mul2f2", lambda v, x=e[k] + g[k]: v % P == x * inv_rp_p % P and v < 2 * P))
+    # NTT lazy radix-4 sums (field.hpp add_raw / add_raw_reduce / sub_raw6): inputs < 2m
+    edge4 = [0, 1, R - 1, R, 2 * R - 1]
+    r4 = [[rnd.randrange(2 * R) for _ in range(5)] for _ in range(n)]
+    r4 += [[a, b, c, d, 2 * R - 1] for a in edge4 for b in edge4 for c in (0, 2 * R - 1) for d in (0, 2 * R - 1)]
+    for x0, x1, x2, x3, wv in r4:
+        lines.append("r4r %s" % " ".join(w8(x) for x in (x0, x1, x2, x3, wv)))
+        s02, s13 = x0 + x2, x1 + x3
+        checks.append(("r4r_sum", lambda v, t=s02 + s13: v % R == t % R and v < 2 * R))
+        checks.append(("r4r_dif", lambda v, t=(s02 - s13) * wv: v % R == t * inv_rp_r % R and v < 2 * R))
     for z in (0, P):
         lines.append("iszq %s" % w8(z)); checks.append(("iszq", lambda v: v == 1))
     out = subprocess.run([BIN], input="\n".join(lines) + "\n", capture_output=True, text=True).stdout.strip().split("\n")

@@ -35,6 +35,11 @@ int main() {
       Fq2 a{rdf<FqCfg>(), rdf<FqCfg>()}, b{rdf<FqCfg>(), rdf<FqCfg>()};
       Fq2 r = mul(a, b); prf(r.c0); printf("\n"); prf(r.c1);
     }
+    else if (o == "r4r") {  // NTT lazy radix-4 stage pair: raw sums x0+x2, x1+x3; prints s02+s13, (s02-s13) w
+      Fr x0 = rdf<FrCfg>(), x1 = rdf<FrCfg>(), x2 = rdf<FrCfg>(), x3 = rdf<FrCfg>(), w = rdf<FrCfg>();
+      const Fr s02 = add_raw(x0, x2), s13 = add_raw(x1, x3);
+      prf(add_raw_reduce(s02, s13)); printf("\n"); prf(mul(sub_raw6(s02, s13), w));
+    }
     else if (o == "mulr") { Fr a = rdf<FrCfg>(), b = rdf<FrCfg>(); prf(mul(a, b)); }
     else if (o == "canonq") { Fq a = rdf<FqCfg>(); prf(canon(a)); }
     else if (o == "iszq") { Fq a = rdf<FqCfg>(); printf("%d", (int)is_zero(a)); }

@@ -294,6 +294,39 @@ ZDEV Fe<C> sub_2x(const Fe<C>& a, const Fe<C>& b, const Fe<C>& c) {
   return cond_sub(cond_sub(s, C::MOD4), C::MOD2);
 }
 
+// ---- lazy radix-4 sums (NTT): a first-stage sum x + y of two normalised values < 2m is kept
+// raw (limbs < 2^30, value < 4m, no carry pass and no conditional subtraction); the second
+// stage consumes two such sums:
+
+// a + b for raw sums a, b < 4m: normalised and reduced from < 8m to < 2m
+template <class C>
+ZDEV Fe<C> add_raw_reduce(const Fe<C>& a, const Fe<C>& b) {
+  Fe<C> s;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) s.v[i] = a.v[i] + b.v[i];
+  normalize(s);
+  return cond_sub(cond_sub(s, C::MOD4), C::MOD2);
+}
+
+// a - b + 6m for raw sums a, b < 4m (wide borrow form: every limb stays >= 0), normalised,
+// value < 10m: an operand of mul() against a normalised value < 2m only (product < 20 m^2)
+template <class C>
+ZDEV Fe<C> sub_raw6(const Fe<C>& a, const Fe<C>& b) {
+  Fe<C> s;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) s.v[i] = a.v[i] + C::MOD6_WIDE[i] - b.v[i];
+  normalize(s);
+  return s;
+}
+
+template <class C>
+ZDEV Fe<C> add_raw(const Fe<C>& a, const Fe<C>& b) {
+  Fe<C> s;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) s.v[i] = a.v[i] + b.v[i];
+  return s;
+}
+
 template <class C>
 ZDEV Fe<C> dbl(const Fe<C>& a) { return add(a, a); }
 

@@ -85,12 +85,19 @@ __device__ __forceinline__ void dft_stages(uint32_t* __restrict__ lds, const uin
       const Fr x0 = lds_get(lds, E, e0), x1 = lds_get(lds, E, e0 + st), x2 = lds_get(lds, E, e0 + 2 * st),
                x3 = lds_get(lds, E, e0 + 3 * st);
       // stage t: (x0, x2) with w_(2H)^i, (x1, x3) with w_(2H)^(i + H/2)
-      const Fr s02 = add(x0, x2), d02 = bfly_d(x0, x2, ltw, i << t);
-      const Fr s13 = add(x1, x3), d13 = bfly_d(x1, x3, ltw, (i + Hh) << t);
+      const Fr d02 = bfly_d(x0, x2, ltw, i << t);
+      const Fr d13 = bfly_d(x1, x3, ltw, (i + Hh) << t);
       // stage t+1: (s02, s13) and (d02, d13), both with w_H^i
       const uint32_t j = i << (t + 1);
-      lds_put(lds, E, e0, add(s02, s13));
-      lds_put(lds, E, e0 + st, bfly_d(s02, s13, ltw, j));
+      if (Hh > 1) {  // the sums stay raw (< 4m) and meet one reduction; w_H^0 = 1 (Montgomery) for i = 0
+        const Fr s02 = add_raw(x0, x2), s13 = add_raw(x1, x3);
+        lds_put(lds, E, e0, add_raw_reduce(s02, s13));
+        lds_put(lds, E, e0 + st, mul(sub_raw6(s02, s13), root(ltw, j)));
+      } else {  // last pair (span 1): no multiply in stage t+1
+        const Fr s02 = add(x0, x2), s13 = add(x1, x3);
+        lds_put(lds, E, e0, add(s02, s13));
+        lds_put(lds, E, e0 + st, sub(s02, s13));
+      }
       lds_put(lds, E, e0 + 2 * st, add(d02, d13));
       lds_put(lds, E, e0 + 3 * st, bfly_d(d02, d13, ltw, j));
     }
