@@ -330,6 +330,9 @@ def main():
         "algorithmic_work_per_launch": {"mixed_adds": int(adds), "fp_mul_per_add": FPMUL_PER_MADD,
                                         "mac_per_fp_mul": MAC_PER_FPMUL},
         "valu_issue_frac_pmc": traffic.get("valu_issue_frac") if traffic else None,
+        # point streaming: PMC HBM bytes per launch over the live average launch time, against 8 TB/s
+        "hbm_GBps": round(traffic["hbm_bytes_per_launch"] / (acc_ms * 1e-3) / 1e9, 1) if (traffic and acc_ms > 0) else None,
+        "hbm_frac_of_8TBps": round(traffic["hbm_bytes_per_launch"] / (acc_ms * 1e-3) / 8e12, 4) if (traffic and acc_ms > 0) else None,
         "note": "integer-multiply (VALU) bound, no MFMA/HBM bound applies (SURVEY.md §8d D3); frac counts the "
                 "algorithmic 136 MAC per Fp mul, the kernel issues ~2.7x that in VALU instructions (29-bit-limb "
                 "FIPS product scanning: 162 mads + carries per mul, plus adds/subs) at valu_issue_frac_pmc of the "

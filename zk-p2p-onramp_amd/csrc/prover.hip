@@ -273,9 +273,15 @@ static void choose_msm_params(size_t n_w, size_t n_h, MsmParams& pw, MsmParams& 
   const int cw = env_int("ZKP_WINDOW_BITS_W", c ? c : clampc(lg(n_w) - 5));
   const int ch = env_int("ZKP_WINDOW_BITS_H", c ? c : clampc(lg(n_h) - 3));
   const int sw = env_int("ZKP_TASK_W", 0), sh = env_int("ZKP_TASK_H", 0);  // entries per task (tuning)
+  // buckets per reduction segment / subset-sum fan-in (tuning; powers of two)
+  const int sm = env_int("ZKP_SEG_M", 0), sl = env_int("ZKP_SUB_L", 0);
   auto tasks = [&] {
     if (sw > 0) pw.S = sw;
     if (sh > 0) ph.S = sh;
+    for (MsmParams* q : {&pw, &ph}) {
+      if (sm > 0 && (sm & (sm - 1)) == 0 && sm <= (1 << (q->c - 1))) q->M = sm;
+      if (sl > 1) q->L = sl;
+    }
   };
   pw = MsmParams::make(n_w, cw, d);
   ph = MsmParams::make(n_h, ch, d);
