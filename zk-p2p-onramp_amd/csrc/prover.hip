@@ -645,7 +645,15 @@ class DevicePipeline {
           }
         }
         HIPX(hipEventRecord(ev_[7], s1_));
-        g2_->run(*plan_w_, *tb2_, wb2);  // finish on s1 too: s3 is in-order, the G1 finishes must not queue behind it
+        // finish on s1 too: s3 is in-order, the G1 finishes must not queue behind it.  With
+        // ZKP_G2_FINISH_GATE=1 the finish (latency-bound merge/reduction chains) waits for the H
+        // plan, so it overlaps the long H accumulation instead of the H plan's sort.
+        g2_->accumulate(*plan_w_, *tb2_);
+        if (!serial_ && g2_finish_gate_) {
+          hdone_f.get();
+          HIPX(hipStreamWaitEvent(s1_, plan_h_->ready(), 0));
+        }
+        g2_->finish(*plan_w_, wb2, s1_);
         HIPX(hipEventRecord(ev_[6], s1_));
       } catch (...) {
         err[1] = std::current_exception();
@@ -720,6 +728,7 @@ class DevicePipeline {
   size_t wlo_ = 0, whi_ = 0, hlo_ = 0, hhi_ = 0;  // witness / domain slice held by this pipeline
   bool serial_ = std::getenv("ZKP_SERIAL") && std::getenv("ZKP_SERIAL")[0] == '1';  // profiling: no stream overlap
   int gate_mode_ = env_int("ZKP_SCHED", 0);
+  bool g2_finish_gate_ = env_int("ZKP_G2_FINISH_GATE", 0) != 0;
   bool sched_gate_ = gate_mode_ != 0;
   ZkeyHeader hdr_;
   hipStream_t s0_ = nullptr, s1_ = nullptr, s2_ = nullptr, s3_ = nullptr;
