@@ -595,6 +595,9 @@ class DevicePipeline {
     std::promise<void> qdone;
     std::shared_future<void> qdone_f = qdone.get_future().share();
     bool qdone_set = false;
+    std::promise<void> g1fin;  // the G1 finishes are enqueued on s3
+    std::shared_future<void> g1fin_f = g1fin.get_future().share();
+    bool g1fin_set = false;
     std::promise<void> hdone;  // H plan enqueued
     std::shared_future<void> hdone_f = hdone.get_future().share();
     bool hdone_set = false;
@@ -626,9 +629,12 @@ class DevicePipeline {
           }
         }
         HIPX(hipEventRecord(ev_[8], s3_));
+        g1fin.set_value();
+        g1fin_set = true;
       } catch (...) {
         err[0] = std::current_exception();
         if (!planned_set) planned.set_exception(std::current_exception());
+        if (!g1fin_set) g1fin.set_exception(std::current_exception());
       }
     };
     auto g2_job = [&] {
@@ -648,13 +654,22 @@ class DevicePipeline {
         // finish on s1 too: s3 is in-order, the G1 finishes must not queue behind it.  With
         // ZKP_G2_FINISH_GATE=1 the finish (latency-bound merge/reduction chains) waits for the H
         // plan, so it overlaps the long H accumulation instead of the H plan's sort.
+        // =2: the gated finish goes to the high-priority finish stream s3 (after the G1 finishes
+        // are enqueued there), so it is not starved by the high-priority H accumulation.
         g2_->accumulate(*plan_w_, *tb2_);
+        hipStream_t fst = s1_;
         if (!serial_ && g2_finish_gate_) {
           hdone_f.get();
-          HIPX(hipStreamWaitEvent(s1_, plan_h_->ready(), 0));
+          if (g2_finish_gate_ == 2) {
+            g1fin_f.get();
+            HIPX(hipEventRecord(ev_[14], s1_));
+            HIPX(hipStreamWaitEvent(s3_, ev_[14], 0));
+            fst = s3_;
+          }
+          HIPX(hipStreamWaitEvent(fst, plan_h_->ready(), 0));
         }
-        g2_->finish(*plan_w_, wb2, s1_);
-        HIPX(hipEventRecord(ev_[6], s1_));
+        g2_->finish(*plan_w_, wb2, fst);
+        HIPX(hipEventRecord(ev_[6], fst));
       } catch (...) {
         err[1] = std::current_exception();
       }
@@ -728,7 +743,7 @@ class DevicePipeline {
   size_t wlo_ = 0, whi_ = 0, hlo_ = 0, hhi_ = 0;  // witness / domain slice held by this pipeline
   bool serial_ = std::getenv("ZKP_SERIAL") && std::getenv("ZKP_SERIAL")[0] == '1';  // profiling: no stream overlap
   int gate_mode_ = env_int("ZKP_SCHED", 0);
-  bool g2_finish_gate_ = env_int("ZKP_G2_FINISH_GATE", 0) != 0;
+  int g2_finish_gate_ = env_int("ZKP_G2_FINISH_GATE", 0);
   bool sched_gate_ = gate_mode_ != 0;
   ZkeyHeader hdr_;
   hipStream_t s0_ = nullptr, s1_ = nullptr, s2_ = nullptr, s3_ = nullptr;
