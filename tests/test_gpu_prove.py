@@ -32,6 +32,24 @@ def test_prove_bit_exact(golden_dir, name):
     assert groth16.js_stringify(res["publicSignals"]) == want_pub
 
 
+# plan / reduction / scheduling variants (read when the prover is built): the compacted H plan
+# instead of the dense one, other bucket-reduction segment sizes and fan-ins, and the
+# scheduling gates -- every variant must give the same golden proof
+KNOBS = [{"ZKP_H_DENSE": "0"}, {"ZKP_SEG_M": "16", "ZKP_SUB_L": "4"}, {"ZKP_SEG_M": "2", "ZKP_SUB_L": "16"},
+         {"ZKP_SCHED": "4"}, {"ZKP_SCHED": "5"}, {"ZKP_G2_FINISH_GATE": "1"}, {"ZKP_G2_FINISH_GATE": "2"}]
+
+
+@pytest.mark.parametrize("knobs", KNOBS, ids=lambda k: ",".join("%s=%s" % kv for kv in k.items()))
+@pytest.mark.parametrize("name", ["small", "venmo_mini"])
+def test_prove_bit_exact_variants(golden_dir, name, knobs, monkeypatch):
+    for k, v in knobs.items():
+        monkeypatch.setenv(k, v)
+    zk, wt = _files(golden_dir, name)
+    man = json.load(open(os.path.join(golden_dir, "manifest.json")))["circuits"][name]
+    res = zkp_amd.Prover(zk).prove(wt, r=int(man["r"]), s=int(man["s"]))
+    assert groth16.js_stringify(res["proof"]) == open(os.path.join(golden_dir, "proof_%s.json" % name)).read()
+
+
 @pytest.mark.parametrize("name", NAMES)
 def test_random_rs_verifies(golden_dir, name):
     zk, wt = _files(golden_dir, name)
