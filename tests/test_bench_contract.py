@@ -1,0 +1,57 @@
+"""The committed bench lines under profiles/ keep the driver's bench.py contract.
+
+Checks the JSON shape the driver parses (metric/value/unit/steps/..., config.workload), that
+`value` is the throughput `ms_per_step` implies, and that the roofline object is internally
+consistent: `achieved` = algorithmic MACs per launch / average launch time (DESIGN.md §5:
+11 Fp-mul per mixed add, 136 MAC per Fp-mul) and `frac` = achieved / peak.
+No GPU and no library needed.
+"""
+import json
+import pathlib
+
+import pytest
+
+PROFILES = pathlib.Path(__file__).resolve().parent.parent / "profiles"
+LINES = ["bench_r01.json", "bench_r01_recheck.json"]
+REQUIRED = ["metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+            "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"]
+
+
+def _load(name):
+    path = PROFILES / name
+    if not path.exists():
+        pytest.skip(f"{name} not committed")
+    return json.loads(path.read_text().strip().splitlines()[-1])
+
+
+@pytest.mark.parametrize("name", LINES)
+def test_contract_keys(name):
+    d = _load(name)
+    for k in REQUIRED:
+        assert k in d, k
+    assert d["unit"] == "proofs/s" and d["higher_is_better"] is True
+    assert d["scaling"] in ("weak", "strong")
+    assert "workload" in d["config"]
+    assert d["n_gpus"] >= 1 and d["steps"] >= 1
+    # whole-job throughput: one proof per step per rank
+    assert d["value"] == pytest.approx(1000.0 * d["n_gpus"] / d["ms_per_step"], rel=0.02)
+
+
+@pytest.mark.parametrize("name", LINES)
+def test_roofline_consistent(name):
+    r = _load(name)["roofline"]
+    for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
+        assert k in r, k
+    assert r["frac"] == pytest.approx(r["achieved"] / r["peak"], rel=1e-3)
+    assert 0.0 < r["frac"] < 1.0
+    w = r["algorithmic_work_per_launch"]
+    mac = w["mixed_adds"] * w["fp_mul_per_add"] * w["mac_per_fp_mul"]
+    assert r["achieved"] == pytest.approx(mac / (r["avg_launch_ms"] * 1e-3) / 1e12, rel=0.01)
+
+
+@pytest.mark.parametrize("name", LINES)
+def test_cpu_baseline(name):
+    c = _load(name)["cpu_baseline"]
+    assert c["kind"] in ("port", "reference")
+    assert c["cores"] >= 1 and c["value"] > 0 and c["sample"]
+    assert c.get("bit_exact_vs_gpu") is True
