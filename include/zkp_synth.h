@@ -23,6 +23,12 @@ typedef struct zkp_synth_circuit zkp_synth_circuit;
 /* 0 on success, nonzero on failure (message via zkp_synth_last_error) */
 int zkp_synth_circuit_new(uint32_t n_vars, uint32_t n_constraints, uint32_t n_public, uint64_t seed,
                           uint32_t in_permille, zkp_synth_circuit** out);
+/* The same with the witness mix as a knob: a defining step is AND (x < bool_percent/2) or XOR
+ * (x < bool_percent), producing a bit, else MUL (a uniform value), for x uniform in [0, 100).
+ * zkp_synth_circuit_new = bool_percent 70 (the Venmo-shape assumption);
+ * 0 = every defined signal uniform (only the input bits stay 0/1). */
+int zkp_synth_circuit_new_mix(uint32_t n_vars, uint32_t n_constraints, uint32_t n_public, uint64_t seed,
+                              uint32_t in_permille, uint32_t bool_percent, zkp_synth_circuit** out);
 void zkp_synth_circuit_free(zkp_synth_circuit* c);
 uint32_t zkp_synth_domain_size(const zkp_synth_circuit* c);
 

@@ -179,3 +179,23 @@ def read_zkey(buf: bytes) -> ZKey:
     h = g1s(9, domain)
     return ZKey(n_vars, n_public, domain, alpha1, beta1, beta2, gamma2, delta1, delta2, ic, coefs,
                 a, b1, b2, c, h)
+
+
+def read_zkey_vk(buf):
+    """Only what verification needs (header points + IC, section 3) from a zkey buffer
+    (bytes or a memoryview over a multi-GB key: nothing else is touched)."""
+    _, secs = read_binfile(buf, b"zkey", 1)
+    o, _ = secs[2][0]
+    o += 4 + 32 + 4 + 32
+    n_vars, n_public, domain = struct.unpack_from("<III", buf, o)
+    o += 12
+    rd1 = lambda off: bn254.g1_from_lem(bytes(buf[off:off + 64]))
+    rd2 = lambda off: bn254.g2_from_lem(bytes(buf[off:off + 128]))
+    alpha1, beta1, beta2 = rd1(o), rd1(o + 64), rd2(o + 128)
+    gamma2, delta1, delta2 = rd2(o + 256), rd1(o + 384), rd2(o + 448)
+    off, ln = secs[3][0]
+    if ln != 64 * (n_public + 1):
+        raise ValueError("zkey: section 3 has wrong size")
+    ic = [rd1(off + 64 * i) for i in range(n_public + 1)]
+    return {"n_vars": n_vars, "n_public": n_public, "domain": domain, "alpha1": alpha1, "beta1": beta1,
+            "beta2": beta2, "gamma2": gamma2, "delta1": delta1, "delta2": delta2, "ic": ic}

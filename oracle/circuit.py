@@ -77,9 +77,12 @@ def _lc(pairs):
     return sorted((s, c) for s, c in d.items() if c != 0)
 
 
-def gen_program(n_vars: int, n_constraints: int, n_public: int, seed: int, in_permille: int = 50):
+def gen_program(n_vars: int, n_constraints: int, n_public: int, seed: int, in_permille: int = 50,
+                bool_pct: int = 70):
     """Circuit STRUCTURE from stream 3 of ``seed``: (R1CS, program).  program is the
-    list of defining steps used by ``gen_witness``; nothing here depends on values."""
+    list of defining steps used by ``gen_witness``; nothing here depends on values.
+    ``bool_pct``: share (percent) of AND/XOR (bit-valued) steps, the witness-mix knob;
+    70 is the default assumption, 0 makes every defined signal a uniform MUL value."""
     rng = SplitMix64(seed, 3)
     n_priv = n_vars - 1 - n_public
     n_in = max(2, n_priv * in_permille // 1000)
@@ -90,10 +93,10 @@ def gen_program(n_vars: int, n_constraints: int, n_public: int, seed: int, in_pe
     prog = []
     for v in range(1 + n_public + n_in, n_vars):
         x = rng.below(100)
-        if x < 70:
+        if x < bool_pct:
             a = bits[rng.below(len(bits))]
             b = bits[rng.below(len(bits))]
-            if x < 35:
+            if x < bool_pct // 2:
                 prog.append((0, a, b))
                 cons.append((_lc([(a, 1)]), _lc([(b, 1)]), _lc([(v, 1)])))
             else:
@@ -140,9 +143,10 @@ def gen_witness(program, wseed: int):
     return w
 
 
-def gen_circuit(n_vars: int, n_constraints: int, n_public: int, seed: int, in_permille: int = 50, wseed=None):
+def gen_circuit(n_vars: int, n_constraints: int, n_public: int, seed: int, in_permille: int = 50, wseed=None,
+                bool_pct: int = 70):
     """Returns (R1CS, witness); the witness uses ``wseed`` (default: ``seed``)."""
-    r1cs, prog = gen_program(n_vars, n_constraints, n_public, seed, in_permille)
+    r1cs, prog = gen_program(n_vars, n_constraints, n_public, seed, in_permille, bool_pct)
     return r1cs, gen_witness(prog, seed if wseed is None else wseed)
 
 

@@ -78,3 +78,15 @@ def test_synth_witness_matches_oracle():
     r1cs, w = circuit.gen_circuit(300, 320, 26, 77, wseed=5)
     assert c.witness(5) == binfile.write_wtns(w)
     assert circuit.check_witness(r1cs, w)
+
+
+@pytest.mark.parametrize("bool_pct", [0, 30, 100])
+def test_synth_witness_mix_matches_oracle(bool_pct):
+    """The witness-mix knob (share of bit-valued AND/XOR steps) of the C++ generator is
+    the oracle's, and the witness still satisfies the circuit."""
+    c = synth.Circuit(300, 320, 26, 78, bool_pct=bool_pct)
+    r1cs, w = circuit.gen_circuit(300, 320, 26, 78, wseed=6, bool_pct=bool_pct)
+    assert c.witness(6) == binfile.write_wtns(w)
+    assert circuit.check_witness(r1cs, w)
+    if bool_pct == 0:  # only the free inputs (5 %), w0 and the public values are small
+        assert sum(1 for x in w if x > 1) > 0.85 * len(w)

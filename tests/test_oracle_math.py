@@ -96,3 +96,15 @@ def test_wtns_zkey_roundtrip_and_errors():
     assert q == R and w2 == [x % R for x in w]
     with pytest.raises(ValueError):
         binfile.read_zkey(b"xkey" + zb[4:])
+
+
+def test_read_zkey_vk_matches_full_reader(golden_dir):
+    """The header-only reader the full-size GPU tests verify with (memoryview over a multi-GB
+    key) returns the full reader's verification key."""
+    from oracle import binfile
+    buf = open(os.path.join(golden_dir, "circuit_small.zkey"), "rb").read()
+    z = binfile.read_zkey(buf)
+    vk = binfile.read_zkey_vk(memoryview(buf))
+    assert (vk["alpha1"], vk["beta2"], vk["gamma2"], vk["delta2"], vk["ic"]) == (z.alpha1, z.beta2, z.gamma2,
+                                                                                 z.delta2, z.ic)
+    assert (vk["n_vars"], vk["n_public"], vk["domain"]) == (z.n_vars, z.n_public, z.domain_size)

@@ -133,3 +133,41 @@ def test_distributed_quotient_exchange_gloo(world, n):
         p.join(60)
         assert p.exitcode == 0
     assert res == {k: True for k in range(world)}
+
+
+def _blind_worker(rank, world, port, q):
+    import torch.distributed as dist
+    from zkp_amd.dist import agree_blinding, all_gather_partials
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        zk, wt, _, _, _ = _case("tiny")
+        parts = all_gather_partials(_oracle_partials(zk, wt, world)[rank], None)
+        r, s = agree_blinding(None, None)  # production: no explicit r, s -> rank 0 draws them once
+        (a, b, c), pub = zkp_amd.proof_combine_raw(zk, parts, wt, r, s)
+        explicit = agree_blinding(7 + rank, 11 + rank)  # explicit values: rank 0's win
+        q.put((rank, (r, s), (a, b, c), pub, explicit))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_split_blinding_agreed_gloo_world2():
+    """SplitProver with r = s = None: every rank assembles the SAME (verifying) proof,
+    because the blinding is drawn on rank 0 and broadcast (zkp_amd.dist.agree_blinding)."""
+    from oracle import binfile, groth16
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_blind_worker, args=(k, 2, port, q)) for k in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    (_, rs0, pr0, pub0, ex0), (_, rs1, pr1, pub1, ex1) = res
+    assert rs0 == rs1 and pr0 == pr1 and ex0 == ex1 == (7, 11)
+    zk, _, _, _, _ = _case("tiny")
+    a, b, c = pr0
+    assert groth16.verify_with_zkey(binfile.read_zkey(zk), pub0, {"A": a, "B": b, "C": c})

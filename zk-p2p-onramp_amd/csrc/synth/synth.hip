@@ -416,7 +416,13 @@ const char* zkp_synth_last_error(void) { return g_err.c_str(); }
 
 int zkp_synth_circuit_new(uint32_t n_vars, uint32_t n_cons, uint32_t n_pub, uint64_t seed, uint32_t in_permille,
                           zkp_synth_circuit** out) {
+  return zkp_synth_circuit_new_mix(n_vars, n_cons, n_pub, seed, in_permille, 70, out);
+}
+
+int zkp_synth_circuit_new_mix(uint32_t n_vars, uint32_t n_cons, uint32_t n_pub, uint64_t seed, uint32_t in_permille,
+                              uint32_t bool_percent, zkp_synth_circuit** out) {
   return guarded([&] {
+    if (bool_percent > 100) throw std::runtime_error("bool_percent must be <= 100");
     auto* c = new zkp_synth_circuit();
     try {
       c->n_vars = n_vars;
@@ -433,10 +439,10 @@ int zkp_synth_circuit_new(uint32_t n_vars, uint32_t n_cons, uint32_t n_pub, uint
       for (uint32_t v = 1 + n_pub + c->n_in; v < n_vars; ++v) {
         const uint64_t x = rng.below(100);
         Step st{};
-        if (x < 70) {
+        if (x < bool_percent) {
           st.a = bits[rng.below(bits.size())];
           st.b = bits[rng.below(bits.size())];
-          st.kind = x < 35 ? 0 : 1;
+          st.kind = x < bool_percent / 2 ? 0 : 1;
           bits.push_back(v);
         } else {
           st.kind = 2;

@@ -26,6 +26,8 @@ LIB_PATH = os.path.join(PKG_ROOT, "lib", "libzkp_amd.so")
 HEADER_PATH = os.path.join(os.path.dirname(PKG_ROOT), "include", "zkp_amd.h")
 
 ZKP_OK = 0
+# BN254 scalar field order r (reference contracts/Verifier.sol:341)
+R_MOD = 0x30644E72E131A029B85045B68181585D2833E84879B9709143E1F593F0000001
 STATUS_NAMES = {
     0: "ZKP_OK", 1: "ZKP_ERR_INVALID_ARG", 2: "ZKP_ERR_IO", 3: "ZKP_ERR_FORMAT", 4: "ZKP_ERR_PROTOCOL",
     5: "ZKP_ERR_CURVE", 6: "ZKP_ERR_WITNESS_LENGTH", 7: "ZKP_ERR_DEVICE", 8: "ZKP_ERR_OUT_OF_MEMORY",

@@ -78,6 +78,23 @@ def all_gather_partials(part: bytes, group=None):
     return [raw[i * PARTIAL_BYTES:(i + 1) * PARTIAL_BYTES] for i in range(world)]
 
 
+def agree_blinding(r=None, s=None, group=None):
+    """The blinding scalars every rank must use for one split proof: rank 0's r / s
+    (drawn from the OS CSPRNG when None) broadcast to every rank, so all ranks assemble
+    the SAME proof.  Explicit values are taken from rank 0 as well."""
+    import secrets
+    from . import R_MOD
+    if dist.get_rank(group) == 0:
+        vals = [int(r) % R_MOD if r is not None else secrets.randbelow(R_MOD),
+                int(s) % R_MOD if s is not None else secrets.randbelow(R_MOD)]
+    else:
+        vals = [0, 0]
+    src = dist.get_global_rank(group, 0) if group is not None else 0
+    obj = [vals]
+    dist.broadcast_object_list(obj, src=src, group=group)
+    return obj[0][0], obj[0][1]
+
+
 class SplitProver:
     """One proof split by point range over the ranks of `group` (one GPU per rank)."""
 
@@ -92,11 +109,11 @@ class SplitProver:
         return self.prover.prove_partial(wtns)
 
     def prove_raw(self, wtns: bytes, r=None, s=None, staged_slot=None):
-        """Every rank returns the same proof tuple (as Prover.prove_raw).  r / s must be
-        equal on all ranks (None draws them per rank: pass explicit values in production
-        so that every rank assembles the same proof, or use rank 0's result)."""
+        """Every rank returns the same proof tuple (as Prover.prove_raw): the blinding r / s
+        is rank 0's (None = drawn once on rank 0 from the CSPRNG), broadcast to all ranks."""
         part = self.prover.prove_partial_staged(staged_slot) if staged_slot is not None else self.partial(wtns)
         parts = all_gather_partials(part, self.group)
+        r, s = agree_blinding(r, s, self.group)
         return proof_combine_raw(self.zkey, parts, wtns, r, s)
 
     def prove_raw_distq(self, wtns: bytes, r=None, s=None, slot: int = 0, staged: bool = False):
@@ -115,4 +132,5 @@ class SplitProver:
         torch.cuda.synchronize()
         part = self.prover.prove_partial_ext_staged(slot, [t.data_ptr() for t in sl])
         parts = all_gather_partials(part, self.group)
+        r, s = agree_blinding(r, s, self.group)
         return proof_combine_raw(self.zkey, parts, wtns, r, s)

@@ -25,6 +25,8 @@ def lib():
         u8p = ctypes.POINTER(ctypes.c_uint8)
         L.zkp_synth_circuit_new.argtypes = [ctypes.c_uint32] * 3 + [ctypes.c_uint64, ctypes.c_uint32,
                                                                      ctypes.POINTER(P)]
+        L.zkp_synth_circuit_new_mix.argtypes = [ctypes.c_uint32] * 3 + [ctypes.c_uint64, ctypes.c_uint32,
+                                                                         ctypes.c_uint32, ctypes.POINTER(P)]
         L.zkp_synth_circuit_free.argtypes = [P]
         L.zkp_synth_circuit_free.restype = None
         L.zkp_synth_domain_size.argtypes = [P]
@@ -49,16 +51,20 @@ def _chk(rc):
 
 
 class Circuit:
-    def __init__(self, n_vars, n_constraints, n_public, seed, in_permille=50):
+    def __init__(self, n_vars, n_constraints, n_public, seed, in_permille=50, bool_pct=70):
+        """bool_pct: percent of bit-valued (AND/XOR) defining steps -- the witness-mix knob
+        (70 = the default assumption; 0 = every defined signal uniform)."""
         h = ctypes.c_void_p()
-        _chk(lib().zkp_synth_circuit_new(n_vars, n_constraints, n_public, seed, in_permille, ctypes.byref(h)))
+        _chk(lib().zkp_synth_circuit_new_mix(n_vars, n_constraints, n_public, seed, in_permille, bool_pct,
+                                             ctypes.byref(h)))
+        self.bool_pct = bool_pct
         self._h = h
         self.n_vars, self.n_constraints, self.n_public = n_vars, n_constraints, n_public
         self.domain_size = lib().zkp_synth_domain_size(h)
 
     @classmethod
-    def venmo(cls, seed=0x5A4B5032):
-        return cls(VENMO["n_vars"], VENMO["n_constraints"], VENMO["n_public"], seed)
+    def venmo(cls, seed=0x5A4B5032, bool_pct=70):
+        return cls(VENMO["n_vars"], VENMO["n_constraints"], VENMO["n_public"], seed, bool_pct=bool_pct)
 
     def __del__(self):
         if getattr(self, "_h", None):
