@@ -42,7 +42,9 @@ typedef enum zkp_status {
 
 /* Opaque prover handle: parsed + validated zkey whose point sections are resident in
  * HBM of every device in the list (uploaded once at load).  Immutable after load;
- * concurrent zkp_prove calls on one handle are safe (serialised per device). */
+ * concurrent zkp_prove calls on one handle are safe: each takes one of two witness
+ * upload slots of its device (its H2D overlaps the proof in flight), the proofs
+ * themselves run one at a time per device (one proof saturates an MI355X). */
 typedef struct zkp_prover zkp_prover;
 
 /* One Groth16 proof: affine coordinates, standard-form LE (the pi_a/pi_b/pi_c of
@@ -105,10 +107,18 @@ zkp_status zkp_prover_info(const zkp_prover* p, uint32_t* n_vars, uint32_t* n_pu
 zkp_status zkp_prove(zkp_prover* p, const uint8_t* wtns, size_t len, const uint8_t* r32, const uint8_t* s32,
                      zkp_proof* out);
 
-/* Prove n witnesses, spread over the prover's devices (one host worker per device).
- * r32s / s32s may be NULL (all random) or arrays of n pointers. */
+/* Prove n witnesses, spread over the prover's devices: a shared queue, two host workers per
+ * device (the next witness's H2D overlaps the current proof), every proof attempted.
+ * r32s / s32s may be NULL (all random) or arrays of n pointers.  Returns ZKP_OK if every
+ * proof succeeded, else the first failing proof's status (message names its index). */
 zkp_status zkp_prove_batch(zkp_prover* p, const uint8_t* const* wtns, const size_t* lens, int n,
                            const uint8_t* const* r32s, const uint8_t* const* s32s, zkp_proof* outs);
+/* The same with a per-proof status array (n entries; proofs with ZKP_OK are valid).  A
+ * device that fails (HIP error) is retired and its witness re-queued to the remaining
+ * devices; an invalid witness fails alone. */
+zkp_status zkp_prove_batch_status(zkp_prover* p, const uint8_t* const* wtns, const size_t* lens, int n,
+                                  const uint8_t* const* r32s, const uint8_t* const* s32s, zkp_proof* outs,
+                                  zkp_status* statuses);
 
 /* Partial MSM sums of this prover's slice for one witness (any prover; a full one
  * reports part 0 of 1). */

@@ -125,3 +125,60 @@ def test_prove_from_chunked_gz_zkey(golden_dir, tmp_path):
     man = json.load(open(os.path.join(golden_dir, "manifest.json")))["circuits"]["small"]
     res = zkp_amd.Prover(str(tmp_path / "circuit.zkey")).prove(wt, r=int(man["r"]), s=int(man["s"]))
     assert groth16.js_stringify(res["proof"]) == open(os.path.join(golden_dir, "proof_small.json")).read()
+
+
+def test_batch_per_proof_status(golden_dir):
+    """zkp_prove_batch_status: a bad witness fails alone (its status), the rest prove."""
+    zk, wt = _files(golden_dir, "small")
+    _, bad = _files(golden_dir, "tiny")  # other circuit: wrong witness length
+    p = zkp_amd.Prover(zk)
+    res, st = p.prove_batch_status_raw([wt, bad, wt, b"garbage!" * 4], [3, 3, 5, 5], [7, 7, 9, 9])
+    assert st == [0, 6, 0, 3]
+    assert res[1] is None and res[3] is None
+    assert res[0] == p.prove_raw(wt, 3, 7) and res[2] == p.prove_raw(wt, 5, 9)
+    with pytest.raises(zkp_amd.ZkpError) as e:  # the all-or-error entry point reports the first failure
+        p.prove_batch_raw([wt, bad], [3, 3], [7, 7])
+    assert e.value.status == 6 and "proof 1" in e.value.message
+
+
+def test_batch_requeues_on_device_failure(golden_dir, monkeypatch):
+    """Two pipelines (both on device 0); the test hook makes pipeline 1 report a device failure
+    on its second proof: its witness is re-queued to pipeline 0, every proof of the batch
+    succeeds bit-exactly, and later single proofs skip the failed pipeline."""
+    monkeypatch.setenv("ZKP_TEST_FAIL_PIPELINE", "1")
+    monkeypatch.setenv("ZKP_TEST_FAIL_AFTER", "1")
+    zk, wt = _files(golden_dir, "small")
+    man = json.load(open(os.path.join(golden_dir, "manifest.json")))["circuits"]["small"]
+    r, s = int(man["r"]), int(man["s"])
+    p = zkp_amd.Prover(zk, devices=[0, 0])
+    n = 12
+    res, st = p.prove_batch_status_raw([wt] * n, [r] * n, [s] * n)
+    assert st == [0] * n
+    want = open(os.path.join(golden_dir, "proof_small.json")).read()
+    for (a, b, c), _ in res:
+        assert groth16.js_stringify(zkp_amd.proof_object(a, b, c)) == want
+    for _ in range(3):  # round-robin now skips the failed pipeline
+        assert groth16.js_stringify(p.prove(wt, r=r, s=s)["proof"]) == want
+
+
+def test_concurrent_prove_on_one_handle(golden_dir):
+    """Two host threads call zkp_prove on one handle at once (each takes an upload slot; the
+    proofs run one at a time on the device): every result equals the sequential one."""
+    import threading
+    zk, wt = _files(golden_dir, "venmo_mini")
+    p = zkp_amd.Prover(zk)
+    want = {k: p.prove_raw(wt, 100 + k, 200 + k) for k in range(8)}
+    got, errs = {}, []
+
+    def run(ks):
+        try:
+            for k in ks:
+                got[k] = p.prove_raw(wt, 100 + k, 200 + k)
+        except Exception as e:  # pragma: no cover - reported below
+            errs.append(e)
+    th = [threading.Thread(target=run, args=(range(i, 8, 2),)) for i in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs and got == want

@@ -50,3 +50,58 @@ def test_node_cli(tmp_path):
     pub = [int(x) for x in json.load(open(tmp_path / "public.json"))]
     assert groth16.verify_with_zkey(z, pub, groth16.proof_from_json_obj(json.load(open(tmp_path / "proof.json"))))
     assert open(tmp_path / "public.json").read() == open(os.path.join(GOLD, "public_tiny.json")).read()
+
+
+def test_addon_exports_prove_batch_and_checks_arguments():
+    r = node("const a=require('./zk-p2p-onramp_amd/js/build/zkp_napi.node');"
+             "const z=require('./zk-p2p-onramp_amd/js/groth16.js');"
+             "let out=[typeof a.proveBatch, typeof z.groth16.proveBatch];"
+             "try{a.proveBatch({}, [])}catch(e){out.push(e.message)}"
+             "console.log(JSON.stringify(out))")
+    assert r.returncode == 0, r.stderr
+    t1, t2, msg = json.loads(r.stdout.strip().splitlines()[-1])
+    assert t1 == t2 == "function" and "invalid or freed prover handle" in msg
+
+
+@pytest.mark.gpu
+def test_node_prove_batch_per_proof_errors():
+    """groth16.proveBatch: every witness proved, a bad witness fails alone (Error with the
+    zkp_status code), good ones bit-exact vs the golden proof at fixed r, s."""
+    man = json.load(open(os.path.join(GOLD, "manifest.json")))["circuits"]["small"]
+    zk = os.path.join(GOLD, "circuit_small.zkey")
+    wt = os.path.join(GOLD, "circuit_small.wtns")
+    bad = os.path.join(GOLD, "circuit_tiny.wtns")  # other circuit: wrong witness length
+    r = node("const z=require('./zk-p2p-onramp_amd/js/groth16.js');"
+             "z.groth16.proveBatch(%r, [%r, %r, {type:'mem', data: require('fs').readFileSync(%r)}], undefined,"
+             " {rs:[%r,%r,%r], ss:[%r,%r,%r]}).then(res=>{"
+             " console.log(JSON.stringify(res.map(x=> x instanceof Error ? {err:x.code} : x.proof)));"
+             " z.release()})" % (zk, wt, bad, wt, man["r"], man["r"], man["r"], man["s"], man["s"], man["s"]))
+    assert r.returncode == 0, r.stderr
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    want = json.load(open(os.path.join(GOLD, "proof_small.json")))
+    assert res[0] == want and res[2] == want and res[1] == {"err": "6"}
+
+
+@pytest.mark.gpu
+def test_node_mem_zkey_resident_and_release_while_in_flight():
+    """A memory zkey ({type:'mem'}, the fullProve path) is loaded once and kept resident
+    (keyed by content hash); release() while proofs are in flight defers the free until
+    they finish (the addon holds the handle), so both proofs still resolve correctly."""
+    man = json.load(open(os.path.join(GOLD, "manifest.json")))["circuits"]["small"]
+    zk = os.path.join(GOLD, "circuit_small.zkey")
+    wt = os.path.join(GOLD, "circuit_small.wtns")
+    r = node("const fs=require('fs');const z=require('./zk-p2p-onramp_amd/js/groth16.js');"
+             "const K={type:'mem',data:fs.readFileSync(%r)}, W={type:'mem',data:fs.readFileSync(%r)};"
+             "const o={r:%r,s:%r};"
+             "(async()=>{"
+             " let t0=Date.now(); const a=await z.groth16.prove(K,W,undefined,o); const t1=Date.now()-t0;"
+             " t0=Date.now(); const b=await z.groth16.prove(K,W,undefined,o); const t2=Date.now()-t0;"
+             " const p=[z.groth16.prove(K,W,undefined,o), z.groth16.prove(K,W,undefined,o)]; z.release();"
+             " const c=await Promise.all(p);"
+             " console.log(JSON.stringify({same:[b,c[0],c[1]].every(x=>JSON.stringify(x.proof)===JSON.stringify(a.proof)),"
+             "  proof:a.proof, t1, t2}));"
+             "})().catch(e=>{console.log(JSON.stringify({err:e.message}));process.exit(1)})"
+             % (zk, wt, man["r"], man["s"]))
+    assert r.returncode == 0, r.stdout + r.stderr
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["same"] and out["proof"] == json.load(open(os.path.join(GOLD, "proof_small.json")))

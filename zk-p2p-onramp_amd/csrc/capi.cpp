@@ -261,8 +261,18 @@ zkp_status zkp_prove(zkp_prover* p, const uint8_t* wtns, size_t len, const uint8
 
 zkp_status zkp_prove_batch(zkp_prover* p, const uint8_t* const* wtns, const size_t* lens, int n,
                            const uint8_t* const* r32s, const uint8_t* const* s32s, zkp_proof* outs) {
+  return zkp_prove_batch_status(p, wtns, lens, n, r32s, s32s, outs, nullptr);
+}
+
+zkp_status zkp_prove_batch_status(zkp_prover* p, const uint8_t* const* wtns, const size_t* lens, int n,
+                                  const uint8_t* const* r32s, const uint8_t* const* s32s, zkp_proof* outs,
+                                  zkp_status* statuses) {
   if (!p || (n > 0 && (!wtns || !lens || !outs)) || n < 0) return fail(ZKP_ERR_INVALID_ARG, "null argument");
-  return guard([&] { p->impl->prove_batch(wtns, lens, n, r32s, s32s, outs); });
+  zkp_status first = ZKP_OK;
+  std::string msg;
+  zkp_status s = guard([&] { first = p->impl->prove_batch(wtns, lens, n, r32s, s32s, outs, statuses, &msg); });
+  if (s != ZKP_OK) return s;
+  return first == ZKP_OK ? ZKP_OK : fail(first, msg);
 }
 
 zkp_status zkp_prove_files(zkp_prover* p, const char* wtns_path, const char* proof_path, const char* public_path) {

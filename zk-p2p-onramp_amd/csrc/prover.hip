@@ -5,6 +5,8 @@
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
+#include <deque>
 #include <cstdlib>
 #include <cstring>
 #include <exception>
@@ -390,7 +392,14 @@ class DevicePipeline {
         launch_convert_coefs(val_[m], c.col.size(), s0_);
       }
     }
-    HIPX(hipMalloc(&wit_, std::max<size_t>((size_t)h.n_vars * 32, 32)));
+    // witness upload slots: each has its own copy stream, so a proof's
+    // witness H2D runs outside the compute lock and overlaps the proof in flight
+    for (int k = 0; k < NUP; ++k) {
+      HIPX(hipMalloc(&up_[k], std::max<size_t>((size_t)h.n_vars * 32, 32)));
+      HIPX(hipStreamCreateWithFlags(&sup_[k], hipStreamNonBlocking));
+      HIPX(hipEventCreate(&upev_[k][0]));
+      HIPX(hipEventCreate(&upev_[k][1]));
+    }
     for (auto& b : abc_) HIPX(hipMalloc(&b, nd_all * 32));
     HIPX(hipMalloc(&pscal_, nd_all * 32));
     ntt_ = std::make_unique<NttEngine>((int)h.log_domain, s0_);
@@ -426,13 +435,19 @@ class DevicePipeline {
     tb2_.reset();
     th_.reset();
     for (void* p : {(void*)rowptr_[0], (void*)rowptr_[1], (void*)col_[0], (void*)col_[1], (void*)val_[0],
-                    (void*)val_[1], (void*)wit_, (void*)abc_[0], (void*)abc_[1], (void*)abc_[2], (void*)pscal_,
+                    (void*)val_[1], (void*)up_[0], (void*)up_[1], (void*)abc_[0], (void*)abc_[1], (void*)abc_[2],
+                    (void*)pscal_,
                     (void*)dwin_})
       if (p) (void)hipFree(p);
     for (uint32_t* p : slots_)
       if (p) (void)hipFree(p);
     if (hwin_) (void)hipHostFree(hwin_);
     for (auto& e : ev_) (void)hipEventDestroy(e);
+    for (int k = 0; k < NUP; ++k) {
+      if (sup_[k]) (void)hipStreamDestroy(sup_[k]);
+      for (auto& e : upev_[k])
+        if (e) (void)hipEventDestroy(e);
+    }
     (void)hipStreamDestroy(s0_);
     (void)hipStreamDestroy(s1_);
     (void)hipStreamDestroy(s2_);
@@ -440,12 +455,70 @@ class DevicePipeline {
     if (s4_) (void)hipStreamDestroy(s4_);
   }
 
-  // witness H2D into dst, bracketed by ev_[0]/ev_[1]
-  void upload(const WtnsView& w, uint32_t* dst) {
-    HIPX(hipEventRecord(ev_[0], s0_));
-    HIPX(hipMemcpyAsync(dst, w.values, (size_t)hdr_.n_vars * 32, hipMemcpyHostToDevice, s0_));
-    HIPX(hipEventRecord(ev_[1], s0_));
+  struct MsmOut {
+    Jac<HFq> a, b1, c, h;
+    Jac<HFq2> b2;
+    float ms[6];
+  };
+
+  // ---- witness upload slots.  acquire_upload() blocks until one of the NUP slots is free;
+  // upload() copies a witness into it on the slot's stream (pageable H2D, the calling thread
+  // waits for it, the compute streams do not); prove_uploaded() then runs the proof on it
+  // under the compute lock.  Two callers (two zkp_prove threads, or the two batch workers of
+  // a device) thus overlap one proof's upload with the other's compute.
+  int acquire_upload() {
+    std::unique_lock<std::mutex> lk(upmu_);
+    upcv_.wait(lk, [&] {
+      for (bool b : upbusy_)
+        if (!b) return true;
+      return false;
+    });
+    for (int k = 0; k < NUP; ++k)
+      if (!upbusy_[k]) {
+        upbusy_[k] = true;
+        return k;
+      }
+    return 0;  // unreachable
   }
+  void release_upload(int k) {
+    {
+      std::lock_guard<std::mutex> lk(upmu_);
+      upbusy_[k] = false;
+    }
+    upcv_.notify_one();
+  }
+  struct UploadSlot {  // RAII: one acquired upload slot
+    DevicePipeline* d;
+    int k;
+    explicit UploadSlot(DevicePipeline* dp) : d(dp), k(dp->acquire_upload()) {}
+    ~UploadSlot() { d->release_upload(k); }
+  };
+  // H2D of a witness into slot k; returns the copy time (ms, HIP events on the slot stream)
+  float upload(int k, const WtnsView& w) {
+    HIPX(hipSetDevice(dev_));
+    HIPX(hipEventRecord(upev_[k][0], sup_[k]));
+    HIPX(hipMemcpyAsync(up_[k], w.values, (size_t)hdr_.n_vars * 32, hipMemcpyHostToDevice, sup_[k]));
+    HIPX(hipEventRecord(upev_[k][1], sup_[k]));
+    HIPX(hipStreamSynchronize(sup_[k]));
+    float ms = 0;
+    HIPX(hipEventElapsedTime(&ms, upev_[k][0], upev_[k][1]));
+    return ms;
+  }
+  MsmOut prove_uploaded(int k, float h2d_ms) {
+    std::lock_guard<std::mutex> lk(mu_);
+    HIPX(hipSetDevice(dev_));
+    maybe_inject_fault();
+    HIPX(hipEventRecord(ev_[0], s0_));
+    HIPX(hipEventRecord(ev_[1], s0_));
+    MsmOut o = prove_dev(up_[k]);
+    o.ms[0] = h2d_ms;
+    return o;
+  }
+  // test hook (ZKP_TEST_FAIL_PIPELINE / ZKP_TEST_FAIL_AFTER, read by Prover): this pipeline
+  // reports a device failure on its (after+1)-th proof and every later one
+  void set_fault_injection(int after) { fail_after_ = after; }
+  bool healthy() const { return healthy_.load(); }
+  void mark_failed() { healthy_.store(false); }
 
   // quotient (rows A4..A8) from a device-resident witness; result scalars in pscal_
   void enqueue_quotient(const uint32_t* d_wit) {
@@ -496,19 +569,14 @@ class DevicePipeline {
   }
 
   void quotient(const WtnsView& w, uint8_t* out) {
+    UploadSlot slot(this);
+    upload(slot.k, w);
     std::lock_guard<std::mutex> lk(mu_);
     HIPX(hipSetDevice(dev_));
-    upload(w, wit_);
-    enqueue_quotient(wit_);
+    enqueue_quotient(up_[slot.k]);
     HIPX(hipMemcpyAsync(out, pscal_, (size_t)hdr_.domain_size * 32, hipMemcpyDeviceToHost, s0_));
     HIPX(hipStreamSynchronize(s0_));
   }
-
-  struct MsmOut {
-    Jac<HFq> a, b1, c, h;
-    Jac<HFq2> b2;
-    float ms[6];
-  };
 
   // Distributed quotient of a split proof, stage 1: buildABC on the
   // witness in `slot`, then the coset extension (rows A5-A7) of the vectors in mask (bit 0
@@ -552,10 +620,9 @@ class DevicePipeline {
   }
 
   MsmOut prove(const WtnsView& w) {
-    std::lock_guard<std::mutex> lk(mu_);
-    HIPX(hipSetDevice(dev_));
-    upload(w, wit_);
-    return prove_dev(wit_);
+    UploadSlot slot(this);
+    const float ms = upload(slot.k, w);
+    return prove_uploaded(slot.k, ms);
   }
 
   MsmOut prove_staged(int slot) {
@@ -753,7 +820,21 @@ class DevicePipeline {
   uint32_t* rowptr_[2] = {nullptr, nullptr};
   uint32_t* col_[2] = {nullptr, nullptr};
   uint32_t* val_[2] = {nullptr, nullptr};
-  uint32_t* wit_ = nullptr;
+  static constexpr int NUP = 2;  // witness upload slots (double buffering)
+  uint32_t* up_[NUP] = {nullptr, nullptr};
+  hipStream_t sup_[NUP] = {nullptr, nullptr};
+  hipEvent_t upev_[NUP][2] = {};
+  std::mutex upmu_;
+  std::condition_variable upcv_;
+  bool upbusy_[NUP] = {false, false};
+  std::atomic<bool> healthy_{true};
+  int fail_after_ = -1, proofs_done_ = 0;
+  void maybe_inject_fault() {
+    if (fail_after_ >= 0 && proofs_done_++ >= fail_after_) {
+      healthy_.store(false);
+      throw HipError(hipErrorLaunchFailure, "injected device failure (ZKP_TEST_FAIL_PIPELINE)", __FILE__, __LINE__);
+    }
+  }
   uint32_t* abc_[3] = {nullptr, nullptr, nullptr};
   uint32_t* pscal_ = nullptr;
   const uint32_t* ext_abc_[3] = {nullptr, nullptr, nullptr};  // set only inside prove_ext_staged
@@ -785,6 +866,21 @@ Prover::Prover(const uint8_t* zkey, size_t len, const std::vector<int>& devices,
     if (d < 0 || d >= ndev) throw ZkpError(ZKP_ERR_INVALID_ARG, "device ordinal out of range");
     devs_.push_back(std::make_unique<DevicePipeline>(d, z, part, nparts));
   }
+  // test hook: pipeline ZKP_TEST_FAIL_PIPELINE reports a device failure after
+  // ZKP_TEST_FAIL_AFTER proofs (exercises the batch re-queue; never set in production)
+  const int fp = env_int("ZKP_TEST_FAIL_PIPELINE", -1);
+  if (fp >= 0 && fp < (int)devs_.size()) devs_[fp]->set_fault_injection(env_int("ZKP_TEST_FAIL_AFTER", 0));
+}
+
+// next healthy pipeline in round-robin order (a pipeline that hit a HIP error is skipped)
+DevicePipeline& Prover::pick_device() {
+  const size_t nd = devs_.size();
+  const unsigned start = rr_.fetch_add(1);
+  for (size_t i = 0; i < nd; ++i) {
+    DevicePipeline& d = *devs_[(start + i) % nd];
+    if (d.healthy()) return d;
+  }
+  throw ZkpError(ZKP_ERR_DEVICE, "every device of this prover has failed");
 }
 
 Prover::~Prover() = default;
@@ -932,8 +1028,14 @@ void Prover::prove(const uint8_t* wtns, size_t len, const uint8_t* r32, const ui
   require_full();
   auto t0 = std::chrono::steady_clock::now();
   WtnsView w = check_wtns(hdr_, wtns, len);
-  DevicePipeline& d = *devs_[rr_.fetch_add(1) % devs_.size()];
-  DevicePipeline::MsmOut m = d.prove(w);
+  DevicePipeline& d = pick_device();
+  DevicePipeline::MsmOut m;
+  try {
+    m = d.prove(w);
+  } catch (const HipError&) {
+    d.mark_failed();
+    throw;
+  }
   auto t1 = std::chrono::steady_clock::now();
   assemble(hdr_, m, w, r32, s32, out);
   auto t2 = std::chrono::steady_clock::now();
@@ -944,31 +1046,102 @@ void Prover::prove(const uint8_t* wtns, size_t len, const uint8_t* r32, const ui
   last_ms_[6] = std::chrono::duration<float, std::milli>(t2 - t0).count();
 }
 
-void Prover::prove_batch(const uint8_t* const* wtns, const size_t* lens, int n, const uint8_t* const* r32s,
-                         const uint8_t* const* s32s, zkp_proof* outs) {
+// Batch scheduler: a shared queue of witness indices; two
+// worker threads per device pipeline (one uploads the next witness into a free upload slot
+// while the other's proof computes), per-proof status, and re-queue on device failure: a
+// worker whose device raises a HIP error puts its witness back at the head of the queue
+// and retires the device; the other devices finish the batch.  A witness that is itself
+// invalid (format, length, curve) fails alone.
+zkp_status Prover::prove_batch(const uint8_t* const* wtns, const size_t* lens, int n, const uint8_t* const* r32s,
+                               const uint8_t* const* s32s, zkp_proof* outs, zkp_status* statuses,
+                               std::string* first_error) {
   require_full();
-  std::atomic<int> next{0};
-  std::vector<std::exception_ptr> errs(devs_.size());
-  std::vector<std::thread> th;
-  for (size_t di = 0; di < devs_.size(); ++di) {
-    th.emplace_back([&, di] {
-      try {
-        for (;;) {
-          const int i = next.fetch_add(1);
-          if (i >= n) break;
-          WtnsView w = check_wtns(hdr_, wtns[i], lens[i]);
-          DevicePipeline::MsmOut m = devs_[di]->prove(w);
-          assemble(hdr_, m, w, r32s ? r32s[i] : nullptr, s32s ? s32s[i] : nullptr, &outs[i]);
-        }
-      } catch (...) {
-        errs[di] = std::current_exception();
-        next.store(n);
+  std::vector<zkp_status> st(n, ZKP_ERR_INTERNAL);
+  std::vector<std::string> msg(n);
+  std::mutex qm;
+  std::condition_variable qcv;
+  std::deque<int> q;
+  for (int i = 0; i < n; ++i) q.push_back(i);
+  int outstanding = n;
+  const size_t nd = devs_.size();
+  auto live_devices = [&] {
+    size_t k = 0;
+    for (auto& d : devs_) k += d->healthy() ? 1 : 0;
+    return k;
+  };
+  auto finish = [&](int i, zkp_status s, const std::string& m) {
+    std::lock_guard<std::mutex> lk(qm);
+    st[i] = s;
+    msg[i] = m;
+    --outstanding;
+    qcv.notify_all();
+  };
+  auto worker = [&](size_t di) {
+    DevicePipeline& d = *devs_[di];
+    for (;;) {
+      int i;
+      {
+        std::unique_lock<std::mutex> lk(qm);
+        qcv.wait(lk, [&] { return !q.empty() || outstanding == 0 || !d.healthy(); });
+        if (q.empty() || !d.healthy()) return;
+        i = q.front();
+        q.pop_front();
       }
-    });
+      WtnsView w;
+      try {
+        w = check_wtns(hdr_, wtns[i], lens[i]);
+      } catch (const ZkpError& e) {
+        finish(i, e.status, e.what());
+        continue;
+      }
+      try {
+        DevicePipeline::MsmOut m = d.prove(w);
+        assemble(hdr_, m, w, r32s ? r32s[i] : nullptr, s32s ? s32s[i] : nullptr, &outs[i]);
+        finish(i, ZKP_OK, "");
+      } catch (const HipError& e) {
+        d.mark_failed();
+        std::lock_guard<std::mutex> lk(qm);
+        if (live_devices() > 0) {
+          q.push_front(i);  // re-queue on a healthy device
+        } else {            // nothing left to run on: fail this and everything queued
+          st[i] = ZKP_ERR_DEVICE;
+          msg[i] = e.what();
+          --outstanding;
+          while (!q.empty()) {
+            st[q.front()] = ZKP_ERR_DEVICE;
+            msg[q.front()] = std::string("no healthy device left: ") + e.what();
+            q.pop_front();
+            --outstanding;
+          }
+        }
+        qcv.notify_all();
+        return;
+      } catch (const ZkpError& e) {
+        finish(i, e.status, e.what());
+      } catch (const std::bad_alloc&) {
+        finish(i, ZKP_ERR_OUT_OF_MEMORY, "host out of memory");
+      } catch (const std::exception& e) {
+        finish(i, ZKP_ERR_INTERNAL, e.what());
+      }
+    }
+  };
+  if (live_devices() == 0) {
+    for (int i = 0; i < n; ++i) st[i] = ZKP_ERR_DEVICE, msg[i] = "every device of this prover has failed";
+  } else {
+    std::vector<std::thread> th;
+    for (size_t di = 0; di < nd; ++di)
+      for (int k = 0; k < 2; ++k) th.emplace_back(worker, di);
+    for (auto& t : th) t.join();
   }
-  for (auto& t : th) t.join();
-  for (auto& e : errs)
-    if (e) std::rethrow_exception(e);
+  zkp_status first = ZKP_OK;
+  for (int i = 0; i < n; ++i) {
+    if (statuses) statuses[i] = st[i];
+    if (st[i] != ZKP_OK && first == ZKP_OK) {
+      first = st[i];
+      if (first_error) *first_error = "proof " + std::to_string(i) + ": " + msg[i];
+    }
+  }
+  return first;
 }
 
 void Prover::quotient(const uint8_t* wtns, size_t len, uint8_t* out) {

@@ -68,8 +68,10 @@ class Prover {
   const ZkeyHeader& header() const { return hdr_; }
   // r32/s32 nullable (CSPRNG).  Thread-safe.
   void prove(const uint8_t* wtns, size_t len, const uint8_t* r32, const uint8_t* s32, zkp_proof* out);
-  void prove_batch(const uint8_t* const* wtns, const size_t* lens, int n, const uint8_t* const* r32s,
-                   const uint8_t* const* s32s, zkp_proof* outs);
+  // every proof is attempted; statuses (nullable) receives each proof's status; returns the
+  // first failing status (ZKP_OK if none) with its message in *first_error
+  zkp_status prove_batch(const uint8_t* const* wtns, const size_t* lens, int n, const uint8_t* const* r32s,
+                         const uint8_t* const* s32s, zkp_proof* outs, zkp_status* statuses, std::string* first_error);
   void quotient(const uint8_t* wtns, size_t len, uint8_t* out);
   void timings(float* ms, int n) const;
   // HBM-resident witnesses (benchmarks time the proof without the PCIe copy)
@@ -93,6 +95,7 @@ class Prover {
 
  private:
   void require_full() const;
+  DevicePipeline& pick_device();
   ZkeyHeader hdr_;
   int part_ = 0, nparts_ = 1;
   std::vector<std::unique_ptr<DevicePipeline>> devs_;

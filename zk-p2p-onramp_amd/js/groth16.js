@@ -7,14 +7,19 @@
  * Same arguments (a path or a fastfile memory descriptor {type:"mem", data}), same
  * Promise<{proof, publicSignals}> result with decimal strings and snarkjs' key order,
  * same Error messages (from the C ABI).  The zkey is loaded once per process and stays
- * resident in HBM (snarkjs re-reads it on every call).  There is no CPU fallback: if
- * the native addon or libzkp_amd.so is missing, require() throws.
+ * resident in HBM (snarkjs re-reads it on every call): a path zkey is keyed by its path, a
+ * memory zkey ({type:"mem"} / Buffer, the fullProve / fastfile path) by the SHA-256 of its
+ * bytes, so repeated proofs with the same in-memory key reuse the resident handle.  There is
+ * no CPU fallback: if the native addon or libzkp_amd.so is missing, require() throws.
  */
+const crypto = require('crypto');
 const fs = require('fs');
 const path = require('path');
 const addon = require(path.join(__dirname, 'build', 'zkp_napi.node'));
 
-const provers = new Map();  // zkey path -> handle
+const provers = new Map();     // zkey path -> handle
+const memProvers = new Map();  // sha256(zkey bytes) -> handle, most recently used last
+const MEM_PROVERS_MAX = 2;     // each holds its key's base tables in HBM (~50 GB for Venmo)
 
 function readInput(x) {
   if (x && typeof x === 'object' && x.type === 'mem') return Buffer.from(x.data.buffer ? x.data : Buffer.from(x.data));
@@ -31,7 +36,21 @@ function proverFor(zkey, devices) {
     }
     return h;
   }
-  return addon.loadProver(readInput(zkey), devices);  // memory zkey: caller-owned lifetime
+  const buf = readInput(zkey);
+  const key = crypto.createHash('sha256').update(buf).digest('hex') + ':' + JSON.stringify(devices || []);
+  let h = memProvers.get(key);
+  if (h) {
+    memProvers.delete(key);  // refresh its LRU position
+  } else {
+    h = addon.loadProver(buf, devices);
+    while (memProvers.size >= MEM_PROVERS_MAX) {  // evict the least recently used key; a proof
+      const [k0, h0] = memProvers.entries().next().value;  // still running on it keeps it alive
+      memProvers.delete(k0);                               // until it finishes (addon refcount)
+      addon.freeProver(h0);
+    }
+  }
+  memProvers.set(key, h);
+  return h;
 }
 
 function toBuf32(v) {
@@ -54,7 +73,10 @@ async function prove(zkeyFileName, witnessFileName, logger, opts) {
   const h = proverFor(zkeyFileName, opts.devices);
   const wtns = readInput(witnessFileName);
   if (logger && logger.debug) logger.debug('zkp_amd: proving on MI355X');
-  const r = await addon.prove(h, wtns, toBuf32(opts.r), toBuf32(opts.s));
+  return toSnarkjs(await addon.prove(h, wtns, toBuf32(opts.r), toBuf32(opts.s)));
+}
+
+function toSnarkjs(r) {
   const proof = {
     pi_a: [r.piA[0], r.piA[1], '1'],
     pi_b: [[r.piB[0][0], r.piB[0][1]], [r.piB[1][0], r.piB[1][1]], ['1', '0']],
@@ -62,8 +84,26 @@ async function prove(zkeyFileName, witnessFileName, logger, opts) {
     protocol: 'groth16',
     curve: 'bn128',
   };
-  if (typeof zkeyFileName !== 'string') addon.freeProver(h);
   return { proof, publicSignals: r.publicSignals };
+}
+
+/**
+ * Many onramp proofs in one call (configs[3] batch): the witnesses are spread over the
+ * prover's devices (opts.devices) by the native batch scheduler, each device overlapping the
+ * next witness's upload with the current proof.  Resolves to one entry per witness:
+ * {proof, publicSignals}, or an Error for a witness that failed (the others still prove).
+ * @param witnesses  array of path | {type:"mem", data} | Buffer
+ * @param opts       {devices?: number[], rs?: (bigint|string)[], ss?: (bigint|string)[]}  (rs/ss: tests only)
+ */
+async function proveBatch(zkeyFileName, witnesses, logger, opts) {
+  opts = opts || {};
+  const h = proverFor(zkeyFileName, opts.devices);
+  const bufs = witnesses.map(readInput);
+  if (logger && logger.debug) logger.debug(`zkp_amd: proving a batch of ${bufs.length} on MI355X`);
+  const rs = opts.rs ? opts.rs.map(toBuf32) : undefined;
+  const ss = opts.ss ? opts.ss.map(toBuf32) : undefined;
+  const res = await addon.proveBatch(h, bufs, rs, ss);
+  return res.map((r) => (r instanceof Error ? r : toSnarkjs(r)));
 }
 
 // `snarkjs zkey export soliditycalldata` text (snarkjs 0.4.22 groth16ExportSolidityCallData,
@@ -97,11 +137,14 @@ function onRampArgs(proof, publicSignals) {
 
 function release() {
   for (const h of provers.values()) addon.freeProver(h);
+  for (const h of memProvers.values()) addon.freeProver(h);
   provers.clear();
+  memProvers.clear();
 }
 
 module.exports = {
-  groth16: { prove },
+  groth16: { prove, proveBatch },
+  proveBatch,
   zKey: { exportSolidityCallData },
   prove,
   exportSolidityCallData,

@@ -10,10 +10,16 @@ export interface Proof {
 }
 export interface ProveOptions { devices?: number[]; r?: bigint | string; s?: bigint | string }
 export interface Logger { debug?(msg: string): void; info?(msg: string): void }
+export interface BatchOptions { devices?: number[]; rs?: (bigint | string)[]; ss?: (bigint | string)[] }
 export declare const groth16: {
   prove(zkeyFileName: Input, witnessFileName: Input, logger?: Logger, opts?: ProveOptions):
     Promise<{ proof: Proof; publicSignals: string[] }>;
+  // one entry per witness: the proof, or an Error (code = zkp_status) for a witness that failed
+  proveBatch(zkeyFileName: Input, witnesses: Input[], logger?: Logger, opts?: BatchOptions):
+    Promise<({ proof: Proof; publicSignals: string[] } | Error)[]>;
 };
+export declare function proveBatch(zkey: Input, witnesses: Input[], logger?: Logger, opts?: BatchOptions):
+  Promise<({ proof: Proof; publicSignals: string[] } | Error)[]>;
 export declare function prove(zkey: Input, wtns: Input, logger?: Logger, opts?: ProveOptions):
   Promise<{ proof: Proof; publicSignals: string[] }>;
 export declare const zKey: {

@@ -6,10 +6,17 @@
  *   loadProver(zkeyPathOrBuffer, devices?)       -> external handle (zkey resident in HBM)
  *   prove(handle, wtnsBuffer, r32?, s32?)        -> Promise<{piA:[x,y], piB:[[x0,x1],[y0,y1]], piC:[x,y],
  *                                                            publicSignals:[...]}> (decimal strings)
+ *   proveBatch(handle, [wtnsBuffer...], rs?, ss?) -> Promise<[result | Error, ...]> (zkp_prove_batch_status:
+ *                                                    every proof attempted, per-proof errors)
  *   freeProver(handle)
  *   version()
- * prove() runs zkp_prove on the libuv threadpool (napi_async_work), so the JS main
+ * prove()/proveBatch() run on the libuv threadpool (napi_async_work), so the JS main
  * thread is never blocked — the same async contract as snarkjs' Promise API.
+ *
+ * Handle lifetime: a job holds a reference on the handle object (no GC finalize while it
+ * runs) and counts itself in the handle's in-flight counter; freeProver() on a handle with
+ * jobs in flight only marks it, and the last job to finish frees the prover.  All of this
+ * runs on the JS main thread (async work complete callbacks included), so no atomics.
  */
 #define NAPI_VERSION 8
 #include <node_api.h>
@@ -27,12 +34,33 @@
     }                                                          \
   } while (0)
 
+typedef struct {
+  zkp_prover* p;
+  int inflight;  /* async jobs running on this handle */
+  int freed;     /* freeProver() called: free when inflight drops to 0 */
+} Slot;
+
+static void slot_release_if_idle(Slot* slot) {
+  if (slot->freed && slot->inflight == 0 && slot->p) {
+    zkp_prover_free(slot->p);
+    slot->p = NULL;
+  }
+}
+
 static void finalize_prover(napi_env env, void* data, void* hint) {
   (void)env, (void)hint;
-  /* explicit freeProver() is the normal path; GC of a live handle frees it too */
-  zkp_prover** slot = (zkp_prover**)data;
-  if (*slot) zkp_prover_free(*slot);
+  /* explicit freeProver() is the normal path; GC of a live handle frees it too (a job in
+   * flight holds a reference on the handle, so this never runs under one) */
+  Slot* slot = (Slot*)data;
+  if (slot->p) zkp_prover_free(slot->p);
   free(slot);
+}
+
+/* the live slot of a handle argument, or NULL (not a handle / already freed) */
+static Slot* get_slot(napi_env env, napi_value v) {
+  Slot* slot = NULL;
+  if (napi_get_value_external(env, v, (void**)&slot) != napi_ok || !slot || !slot->p || slot->freed) return NULL;
+  return slot;
 }
 
 static napi_value throw_status(napi_env env, zkp_status st) {
@@ -88,8 +116,8 @@ static napi_value js_load(napi_env env, napi_callback_info info) {
     st = zkp_prover_load_file(path, ndev ? devs : NULL, ndev, &p);
   }
   if (st != ZKP_OK) return throw_status(env, st);
-  zkp_prover** slot = (zkp_prover**)malloc(sizeof *slot);
-  *slot = p;
+  Slot* slot = (Slot*)calloc(1, sizeof *slot);
+  slot->p = p;
   napi_value ext;
   NAPI_CALL(env, napi_create_external(env, slot, finalize_prover, NULL, &ext));
   return ext;
@@ -99,10 +127,12 @@ static napi_value js_free(napi_env env, napi_callback_info info) {
   size_t argc = 1;
   napi_value argv[1];
   NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
-  zkp_prover** slot;
+  Slot* slot = NULL;
   NAPI_CALL(env, napi_get_value_external(env, argv[0], (void**)&slot));
-  if (*slot) zkp_prover_free(*slot);
-  *slot = NULL;
+  if (slot) {
+    slot->freed = 1;
+    slot_release_if_idle(slot);  /* deferred to the last in-flight job otherwise */
+  }
   return NULL;
 }
 
@@ -110,6 +140,8 @@ typedef struct {
   napi_async_work work;
   napi_deferred deferred;
   napi_ref wtns_ref;
+  napi_ref handle_ref;
+  Slot* slot;
   zkp_prover* p;
   const uint8_t* wtns;
   size_t len;
@@ -196,6 +228,9 @@ static void prove_done(napi_env env, napi_status status, void* data) {
     napi_resolve_deferred(env, j->deferred, res);
   }
   napi_delete_reference(env, j->wtns_ref);
+  j->slot->inflight--;
+  slot_release_if_idle(j->slot);
+  napi_delete_reference(env, j->handle_ref);
   napi_delete_async_work(env, j->work);
   free(j->pub);
   free(j);
@@ -225,13 +260,14 @@ static napi_value js_prove(napi_env env, napi_callback_info info) {
     return NULL;
   }
   ProveJob* j = (ProveJob*)calloc(1, sizeof *j);
-  zkp_prover** slot;
-  if (napi_get_value_external(env, argv[0], (void**)&slot) != napi_ok || !*slot) {
+  Slot* slot = get_slot(env, argv[0]);
+  if (!slot) {
     free(j);
     napi_throw_type_error(env, NULL, "invalid or freed prover handle");
     return NULL;
   }
-  j->p = *slot;
+  j->slot = slot;
+  j->p = slot->p;
   void* data;
   if (napi_get_buffer_info(env, argv[1], &data, &j->len) != napi_ok) {
     free(j);
@@ -251,11 +287,174 @@ static napi_value js_prove(napi_env env, napi_callback_info info) {
   j->pub = (uint8_t*)calloc((size_t)npub + 1, 32);
   j->proof.public_capacity = npub;
   j->proof.public_signals = j->pub;
-  napi_create_reference(env, argv[1], 1, &j->wtns_ref);  /* keep the Buffer alive while proving */
+  napi_create_reference(env, argv[1], 1, &j->wtns_ref);   /* keep the Buffer alive while proving */
+  napi_create_reference(env, argv[0], 1, &j->handle_ref); /* ... and the handle (no finalize) */
+  slot->inflight++;
   napi_value promise, name;
   NAPI_CALL(env, napi_create_promise(env, &j->deferred, &promise));
   NAPI_CALL(env, napi_create_string_utf8(env, "zkp_prove", NAPI_AUTO_LENGTH, &name));
   NAPI_CALL(env, napi_create_async_work(env, NULL, name, prove_exec, prove_done, j, &j->work));
+  NAPI_CALL(env, napi_queue_async_work(env, j->work));
+  return promise;
+}
+
+/* ---- proveBatch: zkp_prove_batch_status over an array of witness Buffers */
+typedef struct {
+  napi_async_work work;
+  napi_deferred deferred;
+  napi_ref arr_ref, handle_ref;
+  Slot* slot;
+  zkp_prover* p;
+  int n;
+  const uint8_t** wtns;
+  size_t* lens;
+  uint8_t *rbuf, *sbuf;            /* n x 32 bytes each, or NULL */
+  const uint8_t **rptr, **sptr;
+  zkp_proof* proofs;
+  uint8_t* pub;                    /* n x npub x 32 */
+  zkp_status* st;
+  zkp_status rc;
+  char err[512];
+} BatchJob;
+
+static void batch_free(BatchJob* j) {
+  free(j->wtns), free(j->lens), free(j->rbuf), free(j->sbuf), free(j->rptr), free(j->sptr);
+  free(j->proofs), free(j->pub), free(j->st);
+  free(j);
+}
+
+static void batch_exec(napi_env env, void* data) {
+  (void)env;
+  BatchJob* j = (BatchJob*)data;
+  j->rc = zkp_prove_batch_status(j->p, j->wtns, j->lens, j->n, (const uint8_t* const*)j->rptr,
+                                 (const uint8_t* const*)j->sptr, j->proofs, j->st);
+  if (j->rc != ZKP_OK) snprintf(j->err, sizeof j->err, "%s", zkp_last_error());
+}
+
+static napi_value proof_object(napi_env env, const zkp_proof* pr, const uint8_t* pub) {
+  napi_value res, pb, pa;
+  napi_create_object(env, &res);
+  napi_set_named_property(env, res, "piA", pair(env, pr->pi_a[0], pr->pi_a[1]));
+  napi_create_array_with_length(env, 2, &pb);
+  napi_set_element(env, pb, 0, pair(env, pr->pi_b[0][0], pr->pi_b[0][1]));
+  napi_set_element(env, pb, 1, pair(env, pr->pi_b[1][0], pr->pi_b[1][1]));
+  napi_set_named_property(env, res, "piB", pb);
+  napi_set_named_property(env, res, "piC", pair(env, pr->pi_c[0], pr->pi_c[1]));
+  napi_create_array_with_length(env, pr->n_public, &pa);
+  for (uint32_t i = 0; i < pr->n_public && i < pr->public_capacity; ++i)
+    napi_set_element(env, pa, i, dec_str(env, pub + 32 * (size_t)i));
+  napi_set_named_property(env, res, "publicSignals", pa);
+  return res;
+}
+
+static void batch_done(napi_env env, napi_status status, void* data) {
+  BatchJob* j = (BatchJob*)data;
+  (void)status;
+  napi_value arr;
+  napi_create_array_with_length(env, (size_t)j->n, &arr);
+  for (int i = 0; i < j->n; ++i) {
+    napi_value v;
+    if (j->st[i] == ZKP_OK) {
+      v = proof_object(env, &j->proofs[i], j->proofs[i].public_signals);
+    } else {
+      napi_value msg, code;
+      char c[16], m[96];
+      snprintf(c, sizeof c, "%d", (int)j->st[i]);
+      snprintf(m, sizeof m, "proof %d failed with status %d", i, (int)j->st[i]);
+      napi_create_string_utf8(env, j->rc != ZKP_OK && j->n == 1 ? j->err : m, NAPI_AUTO_LENGTH, &msg);
+      napi_create_string_utf8(env, c, NAPI_AUTO_LENGTH, &code);
+      napi_create_error(env, code, msg, &v);
+    }
+    napi_set_element(env, arr, (uint32_t)i, v);
+  }
+  napi_resolve_deferred(env, j->deferred, arr);
+  napi_delete_reference(env, j->arr_ref);
+  j->slot->inflight--;
+  slot_release_if_idle(j->slot);
+  napi_delete_reference(env, j->handle_ref);
+  napi_delete_async_work(env, j->work);
+  batch_free(j);
+}
+
+/* rs / ss: undefined or an array of n 32-byte Buffers */
+static int get_scalars(napi_env env, napi_value v, int n, uint8_t** buf, const uint8_t*** ptr) {
+  napi_valuetype t;
+  napi_typeof(env, v, &t);
+  if (t == napi_undefined || t == napi_null) return 0;
+  bool is_arr = false;
+  napi_is_array(env, v, &is_arr);
+  uint32_t len = 0;
+  if (!is_arr || napi_get_array_length(env, v, &len) != napi_ok || (int)len != n) return -1;
+  *buf = (uint8_t*)calloc((size_t)n + 1, 32);
+  *ptr = (const uint8_t**)calloc((size_t)n + 1, sizeof **ptr);
+  for (int i = 0; i < n; ++i) {
+    napi_value e;
+    napi_get_element(env, v, (uint32_t)i, &e);
+    if (get_scalar(env, e, *buf + 32 * (size_t)i) != 1) return -1;
+    (*ptr)[i] = *buf + 32 * (size_t)i;
+  }
+  return 1;
+}
+
+static napi_value js_prove_batch(napi_env env, napi_callback_info info) {
+  size_t argc = 4;
+  napi_value argv[4];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  if (argc < 2) {
+    napi_throw_type_error(env, NULL, "proveBatch(handle, [wtnsBuffer...], rs?, ss?)");
+    return NULL;
+  }
+  Slot* slot = get_slot(env, argv[0]);
+  if (!slot) {
+    napi_throw_type_error(env, NULL, "invalid or freed prover handle");
+    return NULL;
+  }
+  bool is_arr = false;
+  uint32_t n = 0;
+  napi_is_array(env, argv[1], &is_arr);
+  if (!is_arr || napi_get_array_length(env, argv[1], &n) != napi_ok) {
+    napi_throw_type_error(env, NULL, "witnesses must be an array of Buffers");
+    return NULL;
+  }
+  BatchJob* j = (BatchJob*)calloc(1, sizeof *j);
+  j->slot = slot;
+  j->p = slot->p;
+  j->n = (int)n;
+  j->wtns = (const uint8_t**)calloc((size_t)n + 1, sizeof *j->wtns);
+  j->lens = (size_t*)calloc((size_t)n + 1, sizeof *j->lens);
+  for (uint32_t i = 0; i < n; ++i) {
+    napi_value e;
+    void* d;
+    napi_get_element(env, argv[1], i, &e);
+    if (napi_get_buffer_info(env, e, &d, &j->lens[i]) != napi_ok) {
+      batch_free(j);
+      napi_throw_type_error(env, NULL, "witnesses must be an array of Buffers");
+      return NULL;
+    }
+    j->wtns[i] = (const uint8_t*)d;
+  }
+  if ((argc > 2 && get_scalars(env, argv[2], (int)n, &j->rbuf, &j->rptr) < 0) ||
+      (argc > 3 && get_scalars(env, argv[3], (int)n, &j->sbuf, &j->sptr) < 0)) {
+    batch_free(j);
+    napi_throw_type_error(env, NULL, "rs/ss must be arrays of n 32-byte Buffers");
+    return NULL;
+  }
+  uint32_t nv, npub, dom;
+  zkp_prover_info(j->p, &nv, &npub, &dom);
+  j->proofs = (zkp_proof*)calloc((size_t)n + 1, sizeof *j->proofs);
+  j->pub = (uint8_t*)calloc(((size_t)n + 1) * ((size_t)npub + 1), 32);
+  j->st = (zkp_status*)calloc((size_t)n + 1, sizeof *j->st);
+  for (uint32_t i = 0; i < n; ++i) {
+    j->proofs[i].public_capacity = npub;
+    j->proofs[i].public_signals = j->pub + (size_t)i * ((size_t)npub + 1) * 32;
+  }
+  napi_create_reference(env, argv[1], 1, &j->arr_ref);     /* the array keeps every Buffer alive */
+  napi_create_reference(env, argv[0], 1, &j->handle_ref);
+  slot->inflight++;
+  napi_value promise, name;
+  NAPI_CALL(env, napi_create_promise(env, &j->deferred, &promise));
+  NAPI_CALL(env, napi_create_string_utf8(env, "zkp_prove_batch", NAPI_AUTO_LENGTH, &name));
+  NAPI_CALL(env, napi_create_async_work(env, NULL, name, batch_exec, batch_done, j, &j->work));
   NAPI_CALL(env, napi_queue_async_work(env, j->work));
   return promise;
 }
@@ -265,6 +464,7 @@ static napi_value init(napi_env env, napi_value exports) {
       {"version", NULL, js_version, NULL, NULL, NULL, napi_default, NULL},
       {"loadProver", NULL, js_load, NULL, NULL, NULL, napi_default, NULL},
       {"prove", NULL, js_prove, NULL, NULL, NULL, napi_default, NULL},
+      {"proveBatch", NULL, js_prove_batch, NULL, NULL, NULL, napi_default, NULL},
       {"freeProver", NULL, js_free, NULL, NULL, NULL, napi_default, NULL},
   };
   napi_define_properties(env, exports, sizeof props / sizeof props[0], props);

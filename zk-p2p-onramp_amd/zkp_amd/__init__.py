@@ -81,6 +81,9 @@ def load_library(path: str = LIB_PATH):
         lib.zkp_prove.argtypes = [P, u8p, sz, u8p, u8p, ctypes.POINTER(_Proof)]
         lib.zkp_prove_batch.argtypes = [P, ctypes.POINTER(u8p), ctypes.POINTER(sz), ctypes.c_int,
                                         ctypes.POINTER(u8p), ctypes.POINTER(u8p), ctypes.POINTER(_Proof)]
+        lib.zkp_prove_batch_status.argtypes = [P, ctypes.POINTER(u8p), ctypes.POINTER(sz), ctypes.c_int,
+                                               ctypes.POINTER(u8p), ctypes.POINTER(u8p), ctypes.POINTER(_Proof),
+                                               ctypes.POINTER(ctypes.c_int)]
         lib.zkp_prove_files.argtypes = [P, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p]
         lib.zkp_proof_json.argtypes = [ctypes.POINTER(_Proof), ctypes.c_char_p, sz, ctypes.POINTER(sz)]
         lib.zkp_public_json.argtypes = [ctypes.POINTER(_Proof), ctypes.c_char_p, sz, ctypes.POINTER(sz)]
@@ -121,7 +124,7 @@ def load_library(path: str = LIB_PATH):
         lib.zkp_quotient_part_staged.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.POINTER(P)]
         lib.zkp_prove_partial_ext_staged.argtypes = [P, ctypes.c_int, ctypes.POINTER(P), ctypes.c_char_p]
         for name in ("zkp_prover_load_mem", "zkp_prover_load_file", "zkp_prover_info", "zkp_prove",
-                     "zkp_prove_batch", "zkp_prove_files", "zkp_proof_json", "zkp_public_json",
+                     "zkp_prove_batch", "zkp_prove_batch_status", "zkp_prove_files", "zkp_proof_json", "zkp_public_json",
                      "zkp_prover_timings", "zkp_msm_g1", "zkp_msm_g2", "zkp_ntt_fr", "zkp_quotient",
                      "zkp_witness_stage", "zkp_prove_staged", "zkp_prover_instrument", "zkp_prover_kernel_stats",
                      "zkp_bench_msm", "zkp_bench_ntt", "zkp_msm", "zkp_prover_msm_config",
@@ -238,11 +241,21 @@ class Prover:
         return _unpack_proof(pr, pub)
 
     def prove_batch_raw(self, wtns_list, rs=None, ss=None):
+        """All proofs of a batch (raises ZkpError if any proof failed)."""
+        res, st = self._batch(wtns_list, rs, ss, raise_first=True)
+        return res
+
+    def prove_batch_status_raw(self, wtns_list, rs=None, ss=None):
+        """(results, statuses): results[i] is None where statuses[i] != 0 (zkp_prove_batch_status:
+        every proof attempted, device failures re-queued to the remaining devices)."""
+        return self._batch(wtns_list, rs, ss, raise_first=False)
+
+    def _batch(self, wtns_list, rs, ss, raise_first):
         lib = load_library()
         n = len(wtns_list)
         keep = []
-        wps = (ctypes.POINTER(ctypes.c_uint8) * n)()
-        lens = (ctypes.c_size_t * n)()
+        wps = (ctypes.POINTER(ctypes.c_uint8) * max(1, n))()
+        lens = (ctypes.c_size_t * max(1, n))()
         for i, w in enumerate(wtns_list):
             p, k = _buf(w)
             keep.append(k)
@@ -252,7 +265,7 @@ class Prover:
         def arr(vals):
             if vals is None:
                 return None
-            a = (ctypes.POINTER(ctypes.c_uint8) * n)()
+            a = (ctypes.POINTER(ctypes.c_uint8) * max(1, n))()
             for i, v in enumerate(vals):
                 p, k = _buf(int(v).to_bytes(32, "little"))
                 keep.append(k)
@@ -260,15 +273,19 @@ class Prover:
             return a
 
         ra, sa = arr(rs), arr(ss)
-        proofs = (_Proof * n)()
+        proofs = (_Proof * max(1, n))()
         pubs = []
         for i in range(n):
             pub = (ctypes.c_uint8 * (32 * max(1, self.n_public)))()
             pubs.append(pub)
             proofs[i].public_capacity = self.n_public
             proofs[i].public_signals = ctypes.cast(pub, ctypes.POINTER(ctypes.c_uint8))
-        _check(lib.zkp_prove_batch(self._h, wps, lens, n, ra, sa, proofs))
-        return [_unpack_proof(proofs[i], pubs[i]) for i in range(n)]
+        st = (ctypes.c_int * max(1, n))()
+        rc = lib.zkp_prove_batch_status(self._h, wps, lens, n, ra, sa, proofs, st)
+        if rc != ZKP_OK and raise_first:
+            _check(rc)
+        statuses = [st[i] for i in range(n)]
+        return [_unpack_proof(proofs[i], pubs[i]) if statuses[i] == ZKP_OK else None for i in range(n)], statuses
 
     def prove(self, wtns: bytes, r=None, s=None):
         """snarkjs-shaped result {"proof": {...}, "publicSignals": [...]} (decimal strings)."""
