@@ -212,6 +212,11 @@ zkp_status zkp_prover_msm_config(const zkp_prover* p, double* out, int n);
  * [4] window bits c, [5] windows.  out/is_inf receive the result (verification). */
 zkp_status zkp_bench_msm(int device, int g2, const uint8_t* points, const uint8_t* scalars, size_t n, int warmup,
                          int iters, double* stats, uint8_t* out, int* is_inf);
+/* ms per MSM plan build (digits, bucket grouping, task offsets) of n scalars (32-byte LE):
+ * window_bits 0 = automatic; dense != 0: every (window, point) digit an entry, grouped by the
+ * hand-written LDS-staged bucket sort (the H MSM's plan), else the compacted witness plan */
+zkp_status zkp_bench_plan(int device, const uint8_t* scalars, size_t n, int window_bits, int dense, int warmup,
+                          int iters, double* ms);
 /* ms per coset-extension (iNTT + coset key + NTT) of 2^log_n Fr elements */
 zkp_status zkp_bench_ntt(int device, int log_n, int warmup, int iters, double* ms);
 

@@ -87,6 +87,54 @@ def test_msm_g1_bucket_binning(monkeypatch):
         assert zkp_amd.msm_g1(pb, sb, window_bits=c, table_depth=d) == groth16.msm_g1(p, s), (c, d)
 
 
+def test_msm_g1_dense_counting_sort(monkeypatch):
+    # the dense plan (every (window, point) digit an entry, zero digits dropped) grouped by the
+    # hand-written two-level counting sort (k_dsort_*): uniform, skewed (one bucket), sparse,
+    # degenerate, multi-group and every-window-bits inputs against the oracle
+    monkeypatch.setenv("ZKP_MSM_DENSE", "1")
+    pts = _pts(300, 43)
+    rng = circuit.SplitMix64(44, 1)
+    uni = [rng.fr() for _ in range(300)]
+    cases = [
+        (pts, uni, 0, 0),
+        (pts, uni, 20, 0),                            # the H plan's window bits: 2^19 buckets, fine bits 10
+        (pts, uni, 24, 0),                            # fine bits 14 (the largest LDS histogram)
+        (pts, uni, 8, 0), (pts, uni, 9, 0),           # W = 32 / 29 windows: one scalar per thread per round
+        (pts, uni, 6, 4),                             # 2 bucket groups (bucket count not a power of two)
+        (pts, [1] * 150 + uni[:150], 0, 0),           # half the entries in one bucket
+        (pts, [1] * 300, 16, 0),
+        ([pts[0]] * 300, list(range(1, 301)), 0, 0),  # doublings inside buckets
+        (pts, [0] * 299 + [5], 0, 0),
+        (pts, [0] * 300, 0, 0),
+        (pts[:1], [0], 0, 0),
+        (pts[:8], [R + 5, 2 * R + 1, (1 << 256) - 1, R, R - 1, 1, 2, 3], 0, 0),
+    ]
+    for p, s, c, d in cases:
+        pb, sb = _blob(p, s)
+        assert zkp_amd.msm_g1(pb, sb, window_bits=c, table_depth=d) == groth16.msm_g1(p, [x % R for x in s]), (c, d)
+
+
+def test_msm_dense_counting_sort_large(monkeypatch):
+    # several scatter workgroups and every coarse bin populated: 2^14 uniform scalars at c = 20 on
+    # the dense plan vs the compacted plan (rocprim sort) of the same input, G1 and G2
+    rng = circuit.SplitMix64(45, 1)
+    n = 1 << 14
+    g = bn254.FixedBase(bn254.G1_GEN)
+    base = [g.mul(rng.fr() or 1) for _ in range(64)]
+    pts = [base[i % 64] for i in range(n)]
+    sc = [rng.fr() for _ in range(n)]
+    pb, sb = _blob(pts, sc)
+    want = zkp_amd.msm_g1(pb, sb, window_bits=20)
+    monkeypatch.setenv("ZKP_MSM_DENSE", "1")
+    assert zkp_amd.msm_g1(pb, sb, window_bits=20) == want
+    assert zkp_amd.msm_g1(pb, sb, window_bits=13) == want
+    # the oracle on the same sum: scalars of equal bases add up
+    acc = [0] * 64
+    for i, x in enumerate(sc):
+        acc[i % 64] = (acc[i % 64] + x) % R
+    assert want == groth16.msm_g1(base, acc)
+
+
 @pytest.mark.parametrize("k", [1, 4, 10, 12])
 def test_ntt_golden(golden_dir, k):
     d = json.load(open(os.path.join(golden_dir, "ntt_%d.json" % k)))

@@ -1,0 +1,9 @@
+# PMC passes over the isolated hand-written H-plan sort (one counter block per pass).
+set -e
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+P="python3 tools/probe/plan_bench.py 23 3 1"
+timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT --output-format csv -d gpurun_out/pmc_plan1 -o run -- $P > gpurun_out/pmc_plan1.log 2>&1
+timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_SALU SQ_LDS_ADDR_CONFLICT --output-format csv -d gpurun_out/pmc_plan2 -o run -- $P > gpurun_out/pmc_plan2.log 2>&1
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_plan3 -o run -- $P > gpurun_out/pmc_plan3.log 2>&1
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_plan4 -o run -- $P > gpurun_out/pmc_plan4.log 2>&1

@@ -92,6 +92,62 @@ __global__ void k_add_co(uint64_t* out, uint32_t seed) {
   out[blockIdx.x * blockDim.x + threadIdx.x] = s;
 }
 
+// 64-bit shift / shift-add and 32-bit bit ops used around every column of the FIPS multiply
+__global__ void k_lshr_b64(uint64_t* out, uint32_t seed) {
+  uint64_t acc[CHAINS];
+#pragma unroll
+  for (int c = 0; c < CHAINS; ++c) acc[c] = ((uint64_t)(threadIdx.x + seed + c) << 33) | 0x12345u;
+  for (int i = 0; i < ITERS; ++i) {
+#pragma unroll
+    for (int c = 0; c < CHAINS; ++c) {
+      uint64_t r;
+      asm volatile("v_lshrrev_b64 %0, 1, %1" : "=v"(r) : "v"(acc[c]));
+      acc[c] = r;
+    }
+  }
+  uint64_t s = 0;
+#pragma unroll
+  for (int c = 0; c < CHAINS; ++c) s ^= acc[c];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+__global__ void k_lshl_add_u64(uint64_t* out, uint32_t seed) {
+  uint64_t acc[CHAINS];
+  const uint64_t b = 0x9e3779b97f4a7c15ull ^ blockIdx.x;
+#pragma unroll
+  for (int c = 0; c < CHAINS; ++c) acc[c] = threadIdx.x + seed + c;
+  for (int i = 0; i < ITERS; ++i) {
+#pragma unroll
+    for (int c = 0; c < CHAINS; ++c) {
+      uint64_t r;
+      asm volatile("v_lshl_add_u64 %0, %1, 0, %2" : "=v"(r) : "v"(acc[c]), "v"(b));
+      acc[c] = r;
+    }
+  }
+  uint64_t s = 0;
+#pragma unroll
+  for (int c = 0; c < CHAINS; ++c) s ^= acc[c];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+#define K32(NAME, ASM)                                                                  \
+  __global__ void NAME(uint64_t* out, uint32_t seed) {                                  \
+    uint32_t b = blockIdx.x ^ 0x9e3779b9u, acc[CHAINS];                                 \
+    _Pragma("unroll") for (int c = 0; c < CHAINS; ++c) acc[c] = threadIdx.x * 2654435761u + seed + c; \
+    for (int i = 0; i < ITERS; ++i) {                                                   \
+      _Pragma("unroll") for (int c = 0; c < CHAINS; ++c) {                              \
+        uint32_t r;                                                                     \
+        asm volatile(ASM : "=v"(r) : "v"(acc[c]), "v"(b));                              \
+        acc[c] = r;                                                                     \
+      }                                                                                 \
+    }                                                                                   \
+    uint64_t s = 0;                                                                     \
+    _Pragma("unroll") for (int c = 0; c < CHAINS; ++c) s ^= acc[c];                     \
+    out[blockIdx.x * blockDim.x + threadIdx.x] = s;                                     \
+  }
+K32(k_alignbit, "v_alignbit_b32 %0, %1, %2, 29")
+K32(k_add3, "v_add3_u32 %0, %1, %2, %1")
+K32(k_and, "v_and_b32 %0, %1, %2")
+K32(k_lshr_b32, "v_lshrrev_b32 %0, 29, %1")
+
 // f64 fma for comparison
 __global__ void k_fma_f64(uint64_t* out, uint32_t seed) {
   double acc[CHAINS];
@@ -272,6 +328,12 @@ int main() {
   if (run("v_mul_hi_u32", k_mul_hi, d, blocks, threads)) return 1;
   if (run("v_add_co_u32", k_add_co, d, blocks, threads)) return 1;
   if (run("v_fma_f64", k_fma_f64, d, blocks, threads)) return 1;
+  if (run("v_lshrrev_b64", k_lshr_b64, d, blocks, threads)) return 1;
+  if (run("v_lshl_add_u64", k_lshl_add_u64, d, blocks, threads)) return 1;
+  if (run("v_alignbit_b32", k_alignbit, d, blocks, threads)) return 1;
+  if (run("v_add3_u32", k_add3, d, blocks, threads)) return 1;
+  if (run("v_and_b32", k_and, d, blocks, threads)) return 1;
+  if (run("v_lshrrev_b32", k_lshr_b32, d, blocks, threads)) return 1;
   for (int bm : {1, 2, 4, 8}) { uint64_t* d2; CHK(hipMalloc(&d2, (size_t)prop.multiProcessorCount * bm * 256 * 8)); if (run_mont(d2, prop.multiProcessorCount * bm, 256)) return 1; CHK(hipFree(d2)); }
   for (int bm : {1, 2, 4, 8}) { uint64_t* d2; CHK(hipMalloc(&d2, (size_t)prop.multiProcessorCount * bm * 256 * 8)); if (run_mont29(d2, prop.multiProcessorCount * bm, 256)) return 1; CHK(hipFree(d2)); }
   // summary line consumed by bench.py (profiles/ubench_r01.json): best v_mad_u64_u32 rate over occupancies

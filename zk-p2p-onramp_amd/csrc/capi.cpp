@@ -391,6 +391,13 @@ zkp_status zkp_bench_msm(int device, int g2, const uint8_t* points, const uint8_
   });
 }
 
+zkp_status zkp_bench_plan(int device, const uint8_t* scalars, size_t n, int window_bits, int dense, int warmup,
+                          int iters, double* ms) {
+  if (!scalars || !ms || window_bits < 0 || window_bits == 1 || window_bits > 24)
+    return fail(ZKP_ERR_INVALID_ARG, "bad argument");
+  return guard([&] { *ms = zkp::bench_plan(device, scalars, n, window_bits, dense, warmup, iters); });
+}
+
 zkp_status zkp_bench_ntt(int device, int log_n, int warmup, int iters, double* ms) {
   if (!ms || log_n < 1 || log_n > 27) return fail(ZKP_ERR_INVALID_ARG, "bad argument");
   return guard([&] { *ms = zkp::bench_ntt(device, log_n, warmup, iters); });

@@ -361,6 +361,8 @@ __global__ __launch_bounds__(TPB) void k_chunk_bounds(const uint32_t* __restrict
   end[k] = hoff2[base + (size_t)(f + 1) * nch];
 }
 
+#include "hsort_kernels.hpp"
+
 // heavy-merge grid bound per level: heavy c > S2  =>  ceil(c/S2) <= 2c/S2
 inline size_t level_bound(size_t bound, int S2) { return 2 * bound / S2 + 1; }
 
@@ -489,6 +491,38 @@ MsmPlan::MsmPlan(size_t max_n, const MsmParams& prm, hipStream_t stream)
       HIPX(hipMalloc(&hoff2_, nh2 * 4));
     }
   }
+  {
+    int kb = 1;
+    while ((size_t(1) << kb) < nbuckets_) ++kb;
+    hs_b3_ = std::min(kb, HS_B3);
+    hs_b2_ = (kb - hs_b3_) / 2;
+    const int b1 = kb - hs_b3_ - hs_b2_;
+    hs_nbins_ = (uint32_t)((nbuckets_ + (size_t(1) << (hs_b2_ + hs_b3_)) - 1) >> (hs_b2_ + hs_b3_));
+    hs_k_ = std::max(1, std::min(4, HS_STAGE / (HS_TPB * prm_.windows)));
+    if (hs_k_ == 3) hs_k_ = 2;
+    hs_nblk_ = (uint32_t)((max_n_ + hs_k_ * HS_TPB - 1) / (hs_k_ * HS_TPB));
+    hs_max_tiles_ = (uint32_t)((max_entries_ + HS_TILE - 1) / HS_TILE + hs_nbins_);
+    const char* e = std::getenv("ZKP_H_SORT");
+    use_hsort_ = prm_.windows <= HS_STAGE / HS_TPB && b1 <= HS_MAX_B1 && hs_b2_ <= HS_MAX_B2 &&
+                 !(e && std::string(e) == "rocprim");
+    size_t scan_n = nbuckets_ + 1;
+    if (use_hsort_) {
+      const size_t nh = (size_t)hs_nbins_ * hs_nblk_, nh2 = (size_t)hs_max_tiles_ << hs_b2_;
+      HIPX(hipMalloc(&hs_hist_, nh * 4));
+      HIPX(hipMalloc(&hs_blkoff_, nh * 4));
+      HIPX(hipMalloc(&hs_bintot_, (hs_nbins_ + 1) * 4));
+      HIPX(hipMalloc(&hs_binbase_, (hs_nbins_ + 1) * 4));
+      HIPX(hipMalloc(&hs_toff_, (hs_nbins_ + 1) * 4));
+      HIPX(hipMalloc(&hs_hist2_, nh2 * 4));
+      HIPX(hipMalloc(&hs_off2_, nh2 * 4));
+      HIPX(hipMalloc(&hs_subbase_, (((size_t)hs_nbins_ << hs_b2_) + 1) * 4));
+      HIPX(hipMalloc(&hs_ent_a_, max_entries_ * 8));
+      HIPX(hipMalloc(&hs_ent_b_, max_entries_ * 8));
+      scan_n = std::max(scan_n, nh2);
+    }
+    tsum_len_ = scan_tiles_for(scan_n) + 1;
+    HIPX(hipMalloc(&tsum_, tsum_len_ * 4));
+  }
   HIPX(sort_pairs(nullptr, sort_tmp_bytes_, keys_, keys_sorted_, vals_, vals_sorted_, max_entries_, prm_.c - 1,
                   stream_));
   while ((size_t(1) << dense_bits_) <= nbuckets_) ++dense_bits_;
@@ -510,7 +544,9 @@ MsmPlan::~MsmPlan() {
   if (h_valid_) (void)hipHostFree(h_valid_);
   for (void* p : {(void*)keys_, (void*)vals_, (void*)keys_sorted_, (void*)vals_sorted_, (void*)bstart_, (void*)bend_,
                   (void*)cnt_, (void*)off_task_, sort_tmp_, scan_tmp_, (void*)bcnt_, (void*)boff_, (void*)hist_,
-                  (void*)hoff_, (void*)nch_, (void*)choff_, (void*)hist2_, (void*)hoff2_})
+                  (void*)hoff_, (void*)nch_, (void*)choff_, (void*)hist2_, (void*)hoff2_, (void*)hs_hist_,
+                  (void*)hs_blkoff_, (void*)hs_bintot_, (void*)hs_binbase_, (void*)hs_toff_, (void*)hs_hist2_,
+                  (void*)hs_off2_, (void*)hs_subbase_, hs_ent_a_, hs_ent_b_, (void*)tsum_})
     if (p) (void)hipFree(p);
   for (auto* p : off_lvl_)
     if (p) (void)hipFree(p);
@@ -523,7 +559,48 @@ void MsmPlan::build(const uint32_t* scalars, size_t n) {
   const uint32_t nb = (uint32_t)nbuckets_;
   hipStream_t st = stream_;
   total_ = 0;
-  if (dense_ && !use_bins_) {
+  bool counted = false;  // bucket bounds and task counts already written (k_dsort_fine)
+  if (dense_ && use_hsort_ && !use_bins_) {
+    // 1+2. hand-written three-pass bucket sort (hsort_kernels.hpp); total_ = n * W bounds the
+    // nonzero digits (the accumulate grid: threads past the last task exit)
+    total_ = (uint32_t)(n * W);
+    if (total_ == 0) {
+      HIPX(hipMemsetAsync(bstart_, 0, (nbuckets_ + 1) * 4, st));
+      HIPX(hipMemsetAsync(bend_, 0, (nbuckets_ + 1) * 4, st));
+    } else {
+      const int k = hs_k_;
+      const uint32_t nblk = (uint32_t)((n + k * HS_TPB - 1) / (k * HS_TPB)), nsub = 1u << hs_b2_;
+      const int sh1 = hs_b2_ + hs_b3_;
+      uint2* ea = static_cast<uint2*>(hs_ent_a_);
+      uint2* eb = static_cast<uint2*>(hs_ent_b_);
+      // A: digits -> bins
+      auto count1 = k == 4 ? k_hs_count1<4> : (k == 2 ? k_hs_count1<2> : k_hs_count1<1>);
+      hipLaunchKernelGGL(count1, dim3(nblk), dim3(HS_TPB), 0, st, scalars, (uint32_t)n, prm_.c, (int)W, prm_.depth,
+                         sh1, hs_nbins_, hs_hist_);
+      hipLaunchKernelGGL(k_hs_binscan, dim3(hs_nbins_), dim3(HS_TPB), 0, st, hs_hist_, nblk, hs_blkoff_, hs_bintot_);
+      hipLaunchKernelGGL(k_hs_binbase, dim3(1), dim3(512), 0, st, hs_bintot_, hs_nbins_, hs_binbase_, hs_toff_);
+      auto scatter1 = k == 4 ? k_hs_scatter1<4> : (k == 2 ? k_hs_scatter1<2> : k_hs_scatter1<1>);
+      const size_t lds1 = (size_t)k * HS_TPB * W * 8 + (size_t)hs_nbins_ * 8;
+      hipLaunchKernelGGL(scatter1, dim3(nblk), dim3(HS_TPB), lds1, st, scalars, (uint32_t)n, prm_.c, (int)W, prm_.depth,
+                         sh1, hs_nbins_, hs_blkoff_, hs_binbase_, ea);
+      // B: bins -> sub-bins (tiles past the used ones exit; their counters stay zero)
+      const size_t tiles = ((size_t)total_ + HS_TILE - 1) / HS_TILE + hs_nbins_;
+      const size_t nh2 = tiles << hs_b2_;
+      HIPX(hipMemsetAsync(hs_hist2_, 0, nh2 * 4, st));
+      hipLaunchKernelGGL(k_hs_count2, dim3((unsigned)tiles), dim3(HS_TPB), 0, st, ea, hs_binbase_, hs_toff_,
+                         hs_nbins_, hs_b3_, nsub, hs_hist2_);
+      scan_nolookback(hs_hist2_, hs_off2_, nh2, tsum_, st);
+      const uint32_t nq = hs_nbins_ * nsub;
+      hipLaunchKernelGGL(k_hs_subbase, dim3(grid_for(nq + 1)), dim3(HS_TPB), 0, st, hs_off2_, hs_binbase_, hs_toff_,
+                         hs_nbins_, nsub, hs_subbase_);
+      hipLaunchKernelGGL(k_hs_scatter2, dim3((unsigned)tiles), dim3(HS_TPB), 0, st, ea, hs_binbase_, hs_toff_,
+                         hs_nbins_, hs_b3_, nsub, hs_off2_, eb);
+      // C: sub-bins -> buckets, bounds and task counts
+      hipLaunchKernelGGL(k_hs_fine, dim3(nq), dim3(HS_FINE_TPB), 0, st, eb, hs_subbase_, nq, hs_b3_, nb,
+                         (uint32_t)prm_.S, vals_sorted_, bstart_, bend_, cnt_);
+      counted = true;
+    }
+  } else if (dense_ && !use_bins_) {
     // 1+2. dense digits (no compaction) and a full sort on the key bits + sentinel bit
     HIPX(hipMemsetAsync(bstart_, 0, (nbuckets_ + 1) * 4, st));
     HIPX(hipMemsetAsync(bend_, 0, (nbuckets_ + 1) * 4, st));
@@ -593,17 +670,17 @@ void MsmPlan::build(const uint32_t* scalars, size_t n) {
                                             prm_.c - 1, st));
     hipLaunchKernelGGL(k_bounds, dim3(grid_for(total_)), dim3(TPB), 0, st, keys_sorted_, total_, bstart_, bend_);
   }
-  // 3. accumulate-task offsets and the heavy-bucket merge levels' offsets
-  hipLaunchKernelGGL(k_task_counts, dim3(grid_for(nbuckets_ + 1)), dim3(TPB), 0, st, bstart_, bend_, nb,
-                     (uint32_t)prm_.S, cnt_);
-  size_t stmp = scan_tmp_bytes_;
-  HIPX(hipcub::DeviceScan::ExclusiveSum(scan_tmp_, stmp, cnt_, off_task_, (int)(nbuckets_ + 1), st));
+  // 3. accumulate-task offsets and the heavy-bucket merge levels' offsets (look-back-free scans:
+  //    they run beside the accumulations of the other streams)
+  if (!counted)
+    hipLaunchKernelGGL(k_task_counts, dim3(grid_for(nbuckets_ + 1)), dim3(TPB), 0, st, bstart_, bend_, nb,
+                       (uint32_t)prm_.S, cnt_);
+  scan_nolookback(cnt_, off_task_, nbuckets_ + 1, tsum_, st);
   max_tasks_now_ = ((size_t)total_ + prm_.S - 1) / prm_.S + nbuckets_;
   for (int lv = 0; lv < merge_levels_ && total_ > 0; ++lv) {
     hipLaunchKernelGGL(k_heavy_counts, dim3(grid_for(nbuckets_ + 1)), dim3(TPB), 0, st, off_task_, nb,
                        (uint32_t)prm_.S2, lv, cnt_);
-    stmp = scan_tmp_bytes_;
-    HIPX(hipcub::DeviceScan::ExclusiveSum(scan_tmp_, stmp, cnt_, off_lvl_[lv], (int)(nbuckets_ + 1), st));
+    scan_nolookback(cnt_, off_lvl_[lv], nbuckets_ + 1, tsum_, st);
   }
   HIPX(hipGetLastError());
   HIPX(hipEventRecord(ready_, st));

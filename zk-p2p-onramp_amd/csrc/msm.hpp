@@ -164,6 +164,16 @@ class MsmPlan {
   uint32_t *nch_ = nullptr, *choff_ = nullptr, *hist2_ = nullptr, *hoff2_ = nullptr;
   size_t max_chunks_ = 0;
   uint32_t* h_valid_ = nullptr;                 // pinned: number of nonzero digits
+  // dense plans: the hand-written three-pass LDS-staged bucket sort (hsort_kernels.hpp);
+  // ZKP_H_SORT=rocprim restores the onesweep radix sort of the sentinel-keyed digits
+  bool use_hsort_ = false;
+  int hs_b2_ = 0, hs_b3_ = 0, hs_k_ = 1;  // hs_k_: scalars per thread in pass A
+  uint32_t hs_nbins_ = 0, hs_nblk_ = 0, hs_max_tiles_ = 0;
+  uint32_t *hs_hist_ = nullptr, *hs_blkoff_ = nullptr, *hs_bintot_ = nullptr, *hs_binbase_ = nullptr;
+  uint32_t *hs_toff_ = nullptr, *hs_hist2_ = nullptr, *hs_off2_ = nullptr, *hs_subbase_ = nullptr;
+  void *hs_ent_a_ = nullptr, *hs_ent_b_ = nullptr;  // 8-byte (key, base|sign) entries
+  uint32_t* tsum_ = nullptr;                    // tile sums of the look-back-free scans
+  size_t tsum_len_ = 0;
   void* sort_tmp_ = nullptr;
   size_t sort_tmp_bytes_ = 0;
   void* scan_tmp_ = nullptr;

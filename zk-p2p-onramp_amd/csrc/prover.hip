@@ -1233,6 +1233,7 @@ struct MsmRig {
       bases = std::make_unique<MsmBases>(curve, n, prm.c, prm.depth);
       fill_bases(*bases, points, n, 0, st);
       plan = std::make_unique<MsmPlan>(std::max<size_t>(n, 1), prm, st);
+      plan->set_dense(env_int("ZKP_MSM_DENSE", 0) != 0);  // kernel-level MSMs: compacted plan by default
       eng = std::make_unique<MsmEngine>(curve, prm, std::max<size_t>(n, 1), st);
       HIPX(hipMalloc(&ds, std::max<size_t>(n * 32, 32)));
       HIPX(hipMalloc(&dw, eng->window_words() * 4));
@@ -1329,6 +1330,42 @@ MsmBench bench_msm(int device, Curve curve, const uint8_t* points, const uint8_t
   }
   (void)hipEventDestroy(e0), (void)hipEventDestroy(e1);
   return r;
+}
+
+float bench_plan(int device, const uint8_t* scalars, size_t n, int c, int dense, int warmup, int iters) {
+  if (n == 0 || iters <= 0) throw ZkpError(ZKP_ERR_INVALID_ARG, "bench_plan: n and iters must be > 0");
+  HIPX(hipSetDevice(device));
+  hipStream_t st;
+  HIPX(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  uint32_t* d = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  float ms = 0;
+  try {
+    HIPX(hipEventCreate(&e0));
+    HIPX(hipEventCreate(&e1));
+    const MsmParams prm = MsmParams::make(n, c, 0);
+    MsmPlan plan(n, prm, st);
+    plan.set_dense(dense != 0);
+    HIPX(hipMalloc(&d, n * 32));
+    HIPX(hipMemcpyAsync(d, scalars, n * 32, hipMemcpyHostToDevice, st));
+    for (int i = 0; i < warmup; ++i) plan.build(d, n);
+    HIPX(hipStreamSynchronize(st));
+    HIPX(hipEventRecord(e0, st));
+    for (int i = 0; i < iters; ++i) plan.build(d, n);
+    HIPX(hipEventRecord(e1, st));
+    HIPX(hipEventSynchronize(e1));
+    HIPX(hipEventElapsedTime(&ms, e0, e1));
+  } catch (...) {
+    if (d) (void)hipFree(d);
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    (void)hipStreamDestroy(st);
+    throw;
+  }
+  HIPX(hipFree(d));
+  (void)hipEventDestroy(e0), (void)hipEventDestroy(e1);
+  HIPX(hipStreamDestroy(st));
+  return ms / iters;
 }
 
 float bench_ntt(int device, int log_n, int warmup, int iters) {

@@ -130,6 +130,9 @@ struct MsmBench {
 };
 MsmBench bench_msm(int device, Curve curve, const uint8_t* points, const uint8_t* scalars, size_t n, int warmup,
                    int iters, uint8_t* out, int* is_inf);
-float bench_ntt(int device, int log_n, int warmup, int iters);  // ms per coset_extend (iNTT + coset + NTT)
+float bench_ntt(int device, int log_n, int warmup, int iters);
+// ms per MsmPlan::build (digits + bucket grouping + task offsets) of n scalars, window bits c (0 = auto),
+// dense (every digit an entry: the H plan) or compacted
+float bench_plan(int device, const uint8_t* scalars, size_t n, int c, int dense, int warmup, int iters);  // ms per coset_extend (iNTT + coset + NTT)
 
 }  // namespace zkp

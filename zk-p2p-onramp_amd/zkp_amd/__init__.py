@@ -104,6 +104,8 @@ def load_library(path: str = LIB_PATH):
                                       ctypes.POINTER(ctypes.c_double), u8p, ctypes.POINTER(ctypes.c_int)]
         lib.zkp_bench_ntt.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                       ctypes.POINTER(ctypes.c_double)]
+        lib.zkp_bench_plan.argtypes = [ctypes.c_int, u8p, sz, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                       ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
         lib.zkp_msm.argtypes = [ctypes.c_int, ctypes.c_int, u8p, u8p, sz, ctypes.c_int, ctypes.c_int, u8p,
                                 ctypes.POINTER(ctypes.c_int)]
         lib.zkp_prover_msm_config.argtypes = [P, ctypes.POINTER(ctypes.c_double), ctypes.c_int]
@@ -127,7 +129,7 @@ def load_library(path: str = LIB_PATH):
                      "zkp_prove_batch", "zkp_prove_batch_status", "zkp_prove_files", "zkp_proof_json", "zkp_public_json",
                      "zkp_prover_timings", "zkp_msm_g1", "zkp_msm_g2", "zkp_ntt_fr", "zkp_quotient",
                      "zkp_witness_stage", "zkp_prove_staged", "zkp_prover_instrument", "zkp_prover_kernel_stats",
-                     "zkp_bench_msm", "zkp_bench_ntt", "zkp_msm", "zkp_prover_msm_config",
+                     "zkp_bench_msm", "zkp_bench_ntt", "zkp_bench_plan", "zkp_msm", "zkp_prover_msm_config",
                      "zkp_prover_load_part", "zkp_prove_partial", "zkp_proof_calldata",
                      "zkp_prover_load_chunks", "zkp_zkey_read", "zkp_zkey_read_chunks", "zkp_zkey_contribute", "zkp_prove_partial_staged", "zkp_proof_combine",
                      "zkp_quotient_part_staged", "zkp_prove_partial_ext_staged"):
@@ -591,6 +593,16 @@ def bench_msm(points_lem: bytes, scalars_le: bytes, g2: bool = False, warmup: in
     stats = {"ms_per_msm": st[0], "ms_accumulate": st[1], "mixed_adds": int(st[2]), "tasks": int(st[3]),
              "c": int(st[4]), "windows": int(st[5])}
     return stats, res
+
+
+def bench_plan(scalars_le: bytes, window_bits: int = 0, dense: bool = True, warmup: int = 2, iters: int = 10,
+               device: int = 0) -> float:
+    """ms per MSM plan build (digits + bucket grouping + task offsets), device-resident scalars."""
+    ms = ctypes.c_double()
+    sp, sk = _buf(scalars_le)
+    _check(load_library().zkp_bench_plan(device, sp, len(scalars_le) // 32, window_bits, 1 if dense else 0, warmup,
+                                         iters, ctypes.byref(ms)))
+    return ms.value
 
 
 def bench_ntt(log_n: int, warmup: int = 2, iters: int = 10, device: int = 0) -> float:
