@@ -133,6 +133,69 @@ inline void scan_nolookback(const uint32_t* in, uint32_t* out, size_t n, uint32_
   hipLaunchKernelGGL(k_scan_apply, dim3(nt), dim3(SC_TPB), 0, st, in, (uint32_t)n, tsum, out);
 }
 
+// ---------------------------------------------------------------- heavy-bucket merge levels
+// Every merge level's offsets in one go (three launches instead of four per level): level l's
+// count of bucket b is a function of its task count alone (msmk::heavy_counts), so the tiles
+// scan all levels at once; out[l * (nb + 1) + b] = sum over b' < b of level l's counts.
+__device__ __forceinline__ uint32_t lvl_count(uint32_t c0, uint32_t S2, int lvl) {
+  int applied;
+  const uint32_t c = msmk::merged_count(c0, S2, lvl, applied);
+  return (applied == lvl && c > 2 * S2) ? (c + S2 - 1) / S2 : 0u;
+}
+__global__ __launch_bounds__(SC_TPB) void k_lvl_tiles(const uint32_t* __restrict__ off, uint32_t nb, uint32_t S2,
+                                                      int L, uint32_t nt, uint32_t* __restrict__ tsum) {
+  __shared__ uint32_t sh[SC_TPB / 64];
+  const size_t base = (size_t)blockIdx.x * SC_TILE + threadIdx.x * 4;
+  uint32_t c0[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) c0[q] = base + q < nb ? off[base + q + 1] - off[base + q] : 0u;
+  for (int l = 0; l < L; ++l) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v += lvl_count(c0[q], S2, l);
+    uint32_t tot;
+    (void)block_excl_scan<SC_TPB>(v, sh, tot);
+    if (threadIdx.x == 0) tsum[(size_t)l * nt + blockIdx.x] = tot;
+  }
+}
+__global__ __launch_bounds__(SC_TPB) void k_lvl_top(uint32_t* __restrict__ tsum, uint32_t nt) {
+  __shared__ uint32_t sh[SC_TPB / 64];
+  uint32_t* t = tsum + (size_t)blockIdx.x * nt;
+  uint32_t carry = 0;
+  for (uint32_t j0 = 0; j0 < nt; j0 += SC_TPB) {
+    const uint32_t j = j0 + threadIdx.x;
+    const uint32_t v = j < nt ? t[j] : 0u;
+    uint32_t tot;
+    const uint32_t e = block_excl_scan<SC_TPB>(v, sh, tot);
+    if (j < nt) t[j] = carry + e;
+    carry += tot;
+  }
+}
+__global__ __launch_bounds__(SC_TPB) void k_lvl_apply(const uint32_t* __restrict__ off, uint32_t nb, uint32_t S2,
+                                                      int L, uint32_t nt, const uint32_t* __restrict__ tsum,
+                                                      uint32_t* __restrict__ out) {
+  __shared__ uint32_t sh[SC_TPB / 64];
+  const size_t base = (size_t)blockIdx.x * SC_TILE + threadIdx.x * 4;
+  uint32_t c0[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) c0[q] = base + q < nb ? off[base + q + 1] - off[base + q] : 0u;
+  for (int l = 0; l < L; ++l) {
+    uint32_t v[4], run = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      v[q] = lvl_count(c0[q], S2, l);
+      run += v[q];
+    }
+    uint32_t tot;
+    uint32_t e = block_excl_scan<SC_TPB>(run, sh, tot) + tsum[(size_t)l * nt + blockIdx.x];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (base + q <= nb) out[(size_t)l * (nb + 1) + base + q] = e;
+      e += v[q];
+    }
+  }
+}
+
 // ---------------------------------------------------------------- pass A: digits -> bins
 // a workgroup takes K * HS_TPB scalars (K * HS_TPB * W <= HS_STAGE entries), K per thread
 template <int K>
@@ -204,16 +267,27 @@ __global__ __launch_bounds__(HS_TPB) void k_hs_scatter1(const uint32_t* __restri
   __shared__ uint32_t sh[HS_TPB / 64];
   for (uint32_t b = threadIdx.x; b < nbins; b += HS_TPB) cnt[b] = 0;
   __syncthreads();
-  uint32_t s[K][9];
+  // the block's entries stay in registers between the count and the placement (K * W <= EM * K)
+  constexpr int EM = HS_STAGE / HS_TPB / K;
+  constexpr uint32_t NONE = 0xffffffffu;
+  uint2 e[K][EM];
 #pragma unroll
   for (int q = 0; q < K; ++q) {
     const uint32_t i = blockIdx.x * (K * HS_TPB) + q * HS_TPB + threadIdx.x;
-    if (i >= n) continue;
-    msmk::load_scalar(scalars, i, s[q]);
+    uint32_t s[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    const bool act = i < n;
+    if (act) msmk::load_scalar(scalars, i, s);
     uint32_t carry = 0;
-    for (int w = 0; w < W; ++w) {
-      uint32_t key, val;
-      if (msmk::digit_entry(s[q], w, c, T, n, i, carry, key, val)) atomicAdd(&cnt[key >> sh1], 1u);
+#pragma unroll
+    for (int w = 0; w < EM; ++w) {
+      e[q][w] = make_uint2(NONE, 0u);
+      if (w < W) {
+        uint32_t key, val;
+        if (msmk::digit_entry(s, w, c, T, n, i, carry, key, val) && act) {
+          e[q][w] = make_uint2(key, val);
+          atomicAdd(&cnt[key >> sh1], 1u);
+        }
+      }
     }
   }
   __syncthreads();
@@ -223,16 +297,10 @@ __global__ __launch_bounds__(HS_TPB) void k_hs_scatter1(const uint32_t* __restri
   for (uint32_t b = threadIdx.x; b < nbins; b += HS_TPB) cnt[b] = off[b];  // cursors
   __syncthreads();
 #pragma unroll
-  for (int q = 0; q < K; ++q) {
-    const uint32_t i = blockIdx.x * (K * HS_TPB) + q * HS_TPB + threadIdx.x;
-    if (i >= n) continue;
-    uint32_t carry = 0;
-    for (int w = 0; w < W; ++w) {
-      uint32_t key, val;
-      if (msmk::digit_entry(s[q], w, c, T, n, i, carry, key, val))
-        stage[atomicAdd(&cnt[key >> sh1], 1u)] = make_uint2(key, val);
-    }
-  }
+  for (int q = 0; q < K; ++q)
+#pragma unroll
+    for (int w = 0; w < EM; ++w)
+      if (e[q][w].x != NONE) stage[atomicAdd(&cnt[e[q][w].x >> sh1], 1u)] = e[q][w];
   __syncthreads();
   for (uint32_t b = threadIdx.x; b < nbins; b += HS_TPB)  // the cursors become destination bases
     off[b] = binbase[b] + blkoff[(size_t)b * gridDim.x + blockIdx.x] - off[b];

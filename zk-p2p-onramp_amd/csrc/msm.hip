@@ -118,10 +118,6 @@ __global__ __launch_bounds__(TPB) void k_task_counts(const uint32_t* __restrict_
                                                      uint32_t* __restrict__ cnt) {
   msmk::task_counts(blockIdx.x * TPB + threadIdx.x, start, end, nb, S, cnt);
 }
-__global__ __launch_bounds__(TPB) void k_heavy_counts(const uint32_t* __restrict__ off, uint32_t nb, uint32_t S2,
-                                                      int lvl, uint32_t* __restrict__ cnt) {
-  msmk::heavy_counts(blockIdx.x * TPB + threadIdx.x, off, nb, S2, lvl, cnt);
-}
 // G2 (Fq2) accumulation and bucket merges (the wide finish kernels): without a bound the
 // compiler takes 256 VGPRs + AGPRs (one wave per SIMD, nothing to hide the mad-chain
 // latency); two waves per SIMD (a few spilled dwords; accumulation measured 5.24 -> 4.55 ms
@@ -463,7 +459,11 @@ MsmPlan::MsmPlan(size_t max_n, const MsmParams& prm, hipStream_t stream)
   HIPX(hipMalloc(&cnt_, (nbuckets_ + 1) * 4));
   HIPX(hipMalloc(&off_task_, (nbuckets_ + 1) * 4));
   off_lvl_.assign(merge_levels_, nullptr);
-  for (auto& p : off_lvl_) HIPX(hipMalloc(&p, (nbuckets_ + 1) * 4));
+  if (merge_levels_ > 0) {
+    HIPX(hipMalloc(&lvl_all_, (size_t)merge_levels_ * (nbuckets_ + 1) * 4));
+    for (int l = 0; l < merge_levels_; ++l) off_lvl_[l] = lvl_all_ + (size_t)l * (nbuckets_ + 1);
+    HIPX(hipMalloc(&lvl_tsum_, (size_t)merge_levels_ * scan_tiles_for(nbuckets_ + 1) * 4));
+  }
   const size_t ncnt = (size_t)prm_.windows * grid_for(max_n_) + 1;  // per (window, digit block) counts
   HIPX(hipMalloc(&bcnt_, ncnt * 4));
   HIPX(hipMalloc(&boff_, ncnt * 4));
@@ -548,8 +548,8 @@ MsmPlan::~MsmPlan() {
                   (void*)hs_blkoff_, (void*)hs_bintot_, (void*)hs_binbase_, (void*)hs_toff_, (void*)hs_hist2_,
                   (void*)hs_off2_, (void*)hs_subbase_, hs_ent_a_, hs_ent_b_, (void*)tsum_})
     if (p) (void)hipFree(p);
-  for (auto* p : off_lvl_)
-    if (p) (void)hipFree(p);
+  if (lvl_all_) (void)hipFree(lvl_all_);
+  if (lvl_tsum_) (void)hipFree(lvl_tsum_);
 }
 
 void MsmPlan::build(const uint32_t* scalars, size_t n) {
@@ -677,10 +677,13 @@ void MsmPlan::build(const uint32_t* scalars, size_t n) {
                        (uint32_t)prm_.S, cnt_);
   scan_nolookback(cnt_, off_task_, nbuckets_ + 1, tsum_, st);
   max_tasks_now_ = ((size_t)total_ + prm_.S - 1) / prm_.S + nbuckets_;
-  for (int lv = 0; lv < merge_levels_ && total_ > 0; ++lv) {
-    hipLaunchKernelGGL(k_heavy_counts, dim3(grid_for(nbuckets_ + 1)), dim3(TPB), 0, st, off_task_, nb,
-                       (uint32_t)prm_.S2, lv, cnt_);
-    scan_nolookback(cnt_, off_lvl_[lv], nbuckets_ + 1, tsum_, st);
+  if (merge_levels_ > 0 && total_ > 0) {
+    const uint32_t nt = (uint32_t)scan_tiles_for(nbuckets_ + 1);
+    hipLaunchKernelGGL(k_lvl_tiles, dim3(nt), dim3(SC_TPB), 0, st, off_task_, nb, (uint32_t)prm_.S2, merge_levels_,
+                       nt, lvl_tsum_);
+    hipLaunchKernelGGL(k_lvl_top, dim3(merge_levels_), dim3(SC_TPB), 0, st, lvl_tsum_, nt);
+    hipLaunchKernelGGL(k_lvl_apply, dim3(nt), dim3(SC_TPB), 0, st, off_task_, nb, (uint32_t)prm_.S2, merge_levels_,
+                       nt, lvl_tsum_, lvl_all_);
   }
   HIPX(hipGetLastError());
   HIPX(hipEventRecord(ready_, st));

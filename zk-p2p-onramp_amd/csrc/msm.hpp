@@ -152,7 +152,8 @@ class MsmPlan {
   uint32_t total_ = 0;
   uint32_t *keys_ = nullptr, *vals_ = nullptr, *keys_sorted_ = nullptr, *vals_sorted_ = nullptr;
   uint32_t *bstart_ = nullptr, *bend_ = nullptr, *cnt_ = nullptr, *off_task_ = nullptr;
-  std::vector<uint32_t*> off_lvl_;
+  std::vector<uint32_t*> off_lvl_;                // merge level l's offsets: lvl_all_ + l * (buckets + 1)
+  uint32_t *lvl_all_ = nullptr, *lvl_tsum_ = nullptr;
   uint32_t *bcnt_ = nullptr, *boff_ = nullptr;  // per (window, digit block) counts / offsets
   // bucket binning (default grouping): coarse bins x binning blocks counts / offsets
   bool use_bins_ = false;
