@@ -52,12 +52,23 @@ def load_peak():
 
 
 def load_traffic():
-    p = os.path.join(ROOT, "profiles", "pmc_accumulate_r01.json")
-    try:
-        with open(p) as f:
-            return json.load(f)
-    except Exception:
-        return None
+    """Newest committed PMC summary of the accumulate kernel.  HBM bytes per launch = FETCH_SIZE +
+    WRITE_SIZE: the kernel's bytes are random 64-B base gathers, for which FETCH_SIZE counts the
+    bytes exactly (profiles/fetch_calibration_r02.json; the x2 of coalesced 16-B streams does not
+    apply).  Older summaries that stored 2 x FETCH_SIZE are recomputed from their raw counters."""
+    for name in ("pmc_accumulate_r02.json", "pmc_accumulate_r01.json"):
+        p = os.path.join(ROOT, "profiles", name)
+        try:
+            with open(p) as f:
+                d = json.load(f)
+        except Exception:
+            continue
+        g1 = d.get("kernels", {}).get("k_accumulate<Fq >") or d.get("kernels", {}).get("k_accumulate<Fq>")
+        if g1:
+            d["hbm_bytes_per_launch"] = (g1["FETCH_SIZE_kb_avg"] + g1["WRITE_SIZE_kb_avg"]) * 1024
+        d["source"] = "profiles/%s (rocprofv3 --pmc FETCH_SIZE x1 + WRITE_SIZE per launch, gather-calibrated)" % name
+        return d
+    return None
 
 
 def gen_witnesses(circ, seeds):
@@ -442,7 +453,7 @@ def main():
         "unit": "TMAC/s (32x32->64 v_mad_u64_u32)",
         "frac": round(achieved / peak, 4) if (achieved and peak) else None,
         "traffic": traffic.get("hbm_bytes_per_launch") if traffic else None,
-        "traffic_source": "profiles/pmc_accumulate_r01.json (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, per launch)",
+        "traffic_source": traffic.get("source") if traffic else None,
         "algorithmic_work_per_launch": {"mixed_adds": int(adds), "fp_mul_per_add": FPMUL_PER_MADD,
                                         "mac_per_fp_mul": MAC_PER_FPMUL},
         "valu_issue_frac_pmc": traffic.get("valu_issue_frac") if traffic else None,

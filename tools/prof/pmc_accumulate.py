@@ -1,8 +1,10 @@
 #!/usr/bin/env python3
 """Per-launch PMC summary of the bucket-accumulate kernels from three rocprofv3 --pmc
 passes of the same bench command (FETCH_SIZE; WRITE_SIZE; SQ_INSTS_VALU + SQ_WAVES ...).
-HBM bytes per launch = 2 x FETCH_SIZE + WRITE_SIZE (KB units; MI355X_MICROARCH.md HBM
-section: gfx950 FETCH_SIZE reports 1/2 of 16-B/lane loads).  VALU issue fraction =
+HBM bytes per launch = FETCH_SIZE + WRITE_SIZE (KB units).  The guide's x2 on FETCH_SIZE holds for
+coalesced 16-B/lane streams only; the accumulate's bytes are random 64-B base gathers, for which
+FETCH_SIZE reads the bytes exactly (calibrated on a known byte count: profiles/fetch_calibration_r02.json,
+tools/ubench/gather_fetch.hip: gather x1.00, stream x0.50).  VALU issue fraction =
 SQ_INSTS_VALU x 64 lanes / launch time / measured issue peak (35.4 T lane-op/s,
 profiles/ubench_r01.txt: v_mul_lo_u32 / v_add_co_u32).
 usage: pmc_accumulate.py <fetch.csv> <write.csv> <sq.csv> <out.json>"""
@@ -31,8 +33,8 @@ def main(fetch, write, sq, out):
         w = [v for v, _ in W.get(k, {}).get("WRITE_SIZE", [(0, 1)])]
         ins = S.get(k, {}).get("SQ_INSTS_VALU", [])
         e = {"launches": len(f), "FETCH_SIZE_kb_avg": sum(f) / len(f), "WRITE_SIZE_kb_avg": sum(w) / len(w),
-             "hbm_bytes_per_launch": (2 * sum(f) / len(f) + sum(w) / len(w)) * 1024,
-             "correction": "FETCH_SIZE x2 (gfx950, MI355X_MICROARCH.md HBM section), KB units"}
+             "hbm_bytes_per_launch": (sum(f) / len(f) + sum(w) / len(w)) * 1024,
+             "correction": "FETCH_SIZE x1: random 64-B gathers (profiles/fetch_calibration_r02.json), KB units"}
         if ins:
             lane_ops = sum(v * 64 for v, _ in ins) / (sum(ns for _, ns in ins) * 1e-9)
             e.update({"valu_insts_per_launch": sum(v for v, _ in ins) / len(ins),
