@@ -60,6 +60,18 @@ def test_byte_split_chunks_b_to_k_gz(tmp_path):
     assert zkp_amd.read_zkey(str(tmp_path / "circuit.zkey")) == z
 
 
+def test_byte_split_chunks_multi_member(tmp_path):
+    # chunks are inflated in parallel into one buffer sized from the gzip trailers; a chunk of
+    # several gzip members (trailer = last member only) takes the fallback path, same bytes back
+    z = _orig("venmo_mini")
+    step = (len(z) + 3) // 4
+    for i, s in enumerate(SUFFIX[:4]):
+        part = z[i * step:(i + 1) * step]
+        blob = gzip.compress(part[:100]) + gzip.compress(part[100:]) if i == 1 else gzip.compress(part)
+        (tmp_path / ("circuit.zkey%s.gz" % s)).write_bytes(blob)
+    assert zkp_amd.read_zkey(str(tmp_path / "circuit.zkey")) == z
+
+
 def test_section_split_chunks(tmp_path):
     z = _orig("small")
     secs = _sections(z)

@@ -78,6 +78,18 @@ def main(n=300):
         s02, s13 = x0 + x2, x1 + x3
         checks.append(("r4r_sum", lambda v, t=s02 + s13: v % R == t % R and v < 2 * R))
         checks.append(("r4r_dif", lambda v, t=(s02 - s13) * wv: v % R == t * inv_rp_r % R and v < 2 * R))
+    # lazily reduced G1 accumulator x (field.hpp sub_2x8 / lsub8 / canon8, curve.hpp acc_*): a, b, c
+    # < 2m give x < 8m; consumers mul, sqr(lsub8), mul2 with an unnormalised rsub operand
+    x8 = [[rnd.randrange(2 * P) for _ in range(4)] for _ in range(n)]
+    x8 += [[a, b, c, d] for a in edge3 for b in edge3 for c in edge3 for d in (0, 2 * P - 1)]
+    for a, b, c, d in x8:
+        lines.append("x8q %s" % " ".join(w8(x) for x in (a, b, c, d)))
+        x = a - b - 2 * c
+        checks.append(("x8_canon", lambda v, x=x: v % P == x % P and v < 2 * P))
+        checks.append(("x8_mul", lambda v, x=x, d=d: v % P == x * d * inv_rp_p % P and v < 2 * P))
+        checks.append(("x8_lsub8_sqr", lambda v, x=x, d=d: v % P == (d - x) ** 2 * inv_rp_p % P and v < 2 * P))
+        checks.append(("x8_mul2", lambda v, x=x, a=a, b=b, d=d: v % P == (d * (d - x) - a * b) * inv_rp_p % P
+                       and v < 2 * P))
     for z in (0, P):
         lines.append("iszq %s" % w8(z)); checks.append(("iszq", lambda v: v == 1))
     out = subprocess.run([BIN], input="\n".join(lines) + "\n", capture_output=True, text=True).stdout.strip().split("\n")

@@ -40,6 +40,12 @@ int main() {
       const Fr s02 = add_raw(x0, x2), s13 = add_raw(x1, x3);
       prf(add_raw_reduce(s02, s13)); printf("\n"); prf(mul(sub_raw6(s02, s13), w));
     }
+    else if (o == "x8q") {  // lazily reduced accumulator x = a - b - 2c (< 8m) and its consumers
+      Fq a = rdf<FqCfg>(), b = rdf<FqCfg>(), c = rdf<FqCfg>(), d = rdf<FqCfg>();
+      const Fq x = sub_2x8(a, b, c);
+      prf(canon8(x)); printf("\n"); prf(mul(x, d)); printf("\n"); prf(sqr(lsub8(d, x))); printf("\n");
+      prf(mul2(d, lsub8(d, x), a, rsub(fe_zero<FqCfg>(), b)));
+    }
     else if (o == "mulr") { Fr a = rdf<FrCfg>(), b = rdf<FrCfg>(); prf(mul(a, b)); }
     else if (o == "canonq") { Fq a = rdf<FqCfg>(); prf(canon(a)); }
     else if (o == "iszq") { Fq a = rdf<FqCfg>(); printf("%d", (int)is_zero(a)); }
@@ -49,14 +55,14 @@ int main() {
       Xyzz<Fq> acc = xyzz_inf<Fq>();
       xyzz_add_aff(acc, p);
       xyzz_add_aff(acc, q);
-      prf(acc.x); prf(acc.y); prf(acc.zz); prf(acc.zzz);
+      prf(acc_xcanon(acc.x)); prf(acc.y); prf(acc.zz); prf(acc.zzz);
     } else if (o == "g1addx") {  // xyzz + xyzz
       Aff<Fq> p{rdf<FqCfg>(), rdf<FqCfg>()}, q{rdf<FqCfg>(), rdf<FqCfg>()};
       Xyzz<Fq> a = xyzz_inf<Fq>(), b = xyzz_inf<Fq>();
       xyzz_add_aff(a, p); xyzz_add_aff(b, q);
       b = xyzz_dbl(b);
       xyzz_add(a, b);
-      prf(a.x); prf(a.y); prf(a.zz); prf(a.zzz);
+      prf(acc_xcanon(a.x)); prf(a.y); prf(a.zz); prf(a.zzz);
     }
     printf("\n");
     fflush(stdout);

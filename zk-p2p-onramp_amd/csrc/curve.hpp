@@ -39,6 +39,19 @@ ZDEV Fq f_one<Fq>() { return fe_one<FqCfg>(); }
 template <>
 ZDEV Fq2 f_one<Fq2>() { return Fq2{fe_one<FqCfg>(), fe_zero<FqCfg>()}; }
 
+// Accumulator-coordinate forms.  G1: the accumulator x is lazily reduced, < 8m (field.hpp
+// sub_2x8), and the d = 4m - PPP operand of the Y3 sum of products stays unnormalised (rsub:
+// one mul2 operand may have limbs < 2^31, its partner normalised).  G2 keeps canonical
+// coordinates: its Fq2 products need components < 4m.
+ZDEV Fq acc_x3(const Fq& rr, const Fq& ppp, const Fq& q) { return sub_2x8(rr, ppp, q); }
+ZDEV Fq2 acc_x3(const Fq2& rr, const Fq2& ppp, const Fq2& q) { return sub_2x(rr, ppp, q); }
+ZDEV Fq acc_xsub(const Fq& a, const Fq& x) { return lsub8(a, x); }  // a - x for an accumulator x
+ZDEV Fq2 acc_xsub(const Fq2& a, const Fq2& x) { return lsub(a, x); }
+ZDEV Fq acc_negd(const Fq& a) { return rsub(fe_zero<FqCfg>(), a); }
+ZDEV Fq2 acc_negd(const Fq2& a) { return lsub(Fq2{fe_zero<FqCfg>(), fe_zero<FqCfg>()}, a); }
+ZDEV Fq acc_xcanon(const Fq& x) { return canon8(x); }
+ZDEV Fq2 acc_xcanon(const Fq2& x) { return x; }
+
 template <class F>
 ZDEV Xyzz<F> xyzz_inf() {
   Xyzz<F> r;
@@ -114,7 +127,7 @@ ZDEV void xyzz_add_aff(Xyzz<F>& acc, const Aff<F>& q, bool neg = false) {
   const F qy = neg ? rsub(f_zero<F>(), q.y) : q.y;  // mul operand only
   F U2 = mul(q.x, acc.zz);
   F S2 = mul(qy, acc.zzz);
-  F P = lsub(U2, acc.x);
+  F P = acc_xsub(U2, acc.x);
   F R = lsub(S2, acc.y);
   F PP = sqr(P);
   F RR = sqr(R);
@@ -130,8 +143,8 @@ ZDEV void xyzz_add_aff(Xyzz<F>& acc, const Aff<F>& q, bool neg = false) {
   }
   F PPP = mul(P, PP);
   F Q = mul(acc.x, PP);
-  F X3 = sub_2x(RR, PPP, Q);
-  F Y3 = mul2(R, lsub(Q, X3), acc.y, lsub(f_zero<F>(), PPP));  // R (Q - X3) - Y1 PPP
+  F X3 = acc_x3(RR, PPP, Q);
+  F Y3 = mul2(R, acc_xsub(Q, X3), acc.y, acc_negd(PPP));  // R (Q - X3) - Y1 PPP
   acc.zz = mul(acc.zz, PP);
   acc.zzz = mul(acc.zzz, PPP);
   acc.x = X3;
@@ -161,8 +174,8 @@ ZDEV Xyzz<F> xyzz_from_aff_pair(const Aff<F>& p, bool np, const Aff<F>& q, bool 
   }
   F PPP = mul(P, PP);
   F Q = mul(p.x, PP);
-  acc.x = sub_2x(RR, PPP, Q);
-  acc.y = mul2(R, lsub(Q, acc.x), py, lsub(f_zero<F>(), PPP));  // R (Q - X3) - Y1 PPP
+  acc.x = acc_x3(RR, PPP, Q);
+  acc.y = mul2(R, acc_xsub(Q, acc.x), py, acc_negd(PPP));  // R (Q - X3) - Y1 PPP
   acc.zz = PP;
   acc.zzz = PPP;
   return acc;
@@ -193,8 +206,8 @@ ZDEV void xyzz_add(Xyzz<F>& acc, const Xyzz<F>& q) {
   }
   F PPP = mul(P, PP);
   F Q = mul(U1, PP);
-  F X3 = sub_2x(RR, PPP, Q);
-  F Y3 = mul2(R, lsub(Q, X3), S1, lsub(f_zero<F>(), PPP));  // R (Q - X3) - S1 PPP
+  F X3 = acc_x3(RR, PPP, Q);
+  F Y3 = mul2(R, acc_xsub(Q, X3), S1, acc_negd(PPP));  // R (Q - X3) - S1 PPP
   acc.zz = mul(mul(acc.zz, q.zz), PP);
   acc.zzz = mul(mul(acc.zzz, q.zzz), PPP);
   acc.x = X3;
@@ -283,7 +296,7 @@ template <class F>
 ZDEV void store_xyzz(uint32_t* base, size_t idx, const Xyzz<F>& a) {
   constexpr int W = FWords<F>::W;
   uint32_t* p = base + idx * (4 * W);
-  store_f(p, a.x);
+  store_f(p, acc_xcanon(a.x));  // a G1 accumulator x may be < 8m
   store_f(p + W, a.y);
   store_f(p + 2 * W, a.zz);
   store_f(p + 3 * W, a.zzz);

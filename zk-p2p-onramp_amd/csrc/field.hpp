@@ -294,6 +294,35 @@ ZDEV Fe<C> sub_2x(const Fe<C>& a, const Fe<C>& b, const Fe<C>& c) {
   return cond_sub(cond_sub(s, C::MOD4), C::MOD2);
 }
 
+// ---- lazily reduced accumulator x (G1 XYZZ additions): X3 = R^2 - PPP - 2Q stays in (0, 8m)
+// without its two conditional subtractions (~90 instructions per addition).  Every consumer takes
+// an x < 8m: mul()/sqr() operands (the output stays < 2m up to operands of ~11m: a*b/2^261 + m
+// < 2m for a*b < 169 m^2), lsub8() for the differences, canon8() before storage.
+
+// a - b - 2c + 6m for a, b, c < 2m (normalised): normalised, value in (0, 8m)
+template <class C>
+ZDEV Fe<C> sub_2x8(const Fe<C>& a, const Fe<C>& b, const Fe<C>& c) {
+  Fe<C> s;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) s.v[i] = a.v[i] + C::MOD6_WIDE[i] - b.v[i] - (c.v[i] << 1);
+  normalize(s);
+  return s;
+}
+
+// a - b + 8m for a < 2m, b < 8m (normalised): normalised, value < 10m -- a mul / sqr operand
+template <class C>
+ZDEV Fe<C> lsub8(const Fe<C>& a, const Fe<C>& b) {
+  Fe<C> s;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) s.v[i] = a.v[i] + C::MOD8_BORROW[i] - b.v[i];
+  normalize(s);
+  return s;
+}
+
+// x < 8m (normalised) -> < 2m
+template <class C>
+ZDEV Fe<C> canon8(const Fe<C>& a) { return cond_sub(cond_sub(a, C::MOD4), C::MOD2); }
+
 // ---- lazy radix-4 sums (NTT): a first-stage sum x + y of two normalised values < 2m is kept
 // raw (limbs < 2^30, value < 4m, no carry pass and no conditional subtraction); the second
 // stage consumes two such sums:
