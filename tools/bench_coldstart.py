@@ -72,7 +72,7 @@ def main(out=None, work="/tmp/zkp_coldstart"):
     p, res["load_plain_file_s"] = timed(lambda: zkp_amd.Prover(plain, devices=[0]))
     p.close()
     p, res["load_from_memory_s"] = timed(lambda: zkp_amd.Prover(zk, devices=[0]))
-    res["table_bytes_per_device"] = p.msm_config().get("table_bytes_per_device") if hasattr(p, "msm_config") else None
+    res["table_bytes_per_device"] = p.msm_config()["table_bytes_per_device"]
     p.close()
     res["cpu_threads"] = len(os.sched_getaffinity(0))
     res["note"] = ("load_* = zkp_prover_load_file / _mem end to end: read + inflate + merge (host), parse + validate, "
