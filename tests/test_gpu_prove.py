@@ -36,7 +36,7 @@ def test_prove_bit_exact(golden_dir, name):
 # instead of the dense one, the dense plan on the rocprim radix sort instead of the hand-written
 # counting sort, other bucket-reduction segment sizes and fan-ins, and the
 # scheduling gates -- every variant must give the same golden proof
-KNOBS = [{"ZKP_H_DENSE": "0"}, {"ZKP_H_SORT": "rocprim"}, {"ZKP_SEG_M": "16", "ZKP_SUB_L": "4"}, {"ZKP_SEG_M": "2", "ZKP_SUB_L": "16"},
+KNOBS = [{"ZKP_H_DENSE": "0"}, {"ZKP_H_SORT": "rocprim"}, {"ZKP_TASK_ORDER": "bucket"}, {"ZKP_SEG_M": "16", "ZKP_SUB_L": "4"}, {"ZKP_SEG_M": "2", "ZKP_SUB_L": "16"},
          {"ZKP_SCHED": "4"}, {"ZKP_SCHED": "5"}, {"ZKP_G2_FINISH_GATE": "1"}, {"ZKP_G2_FINISH_GATE": "2"}]
 
 

@@ -51,7 +51,7 @@ static host::Jac<HF> run(std::vector<uint32_t>& pts, std::vector<uint32_t>& sc, 
   for (uint32_t b = 0; b <= nb; ++b) { off[b] = acc; acc += cnt[b]; }
   const uint32_t ntask = off[nb];
   std::vector<uint32_t> part((size_t)(ntask + 1) * 4 * FW);
-  for (uint32_t t = 0; t < ntask; ++t) msmk::accumulate<F>(t, table.data(), vs.data(), st.data(), en.data(), off.data(), nb, prm.S, part.data());
+  for (uint32_t t = 0; t < ntask; ++t) msmk::accumulate<F>(t, table.data(), vs.data(), st.data(), en.data(), off.data(), nb, prm.S, nullptr, part.data());
   // heavy-bucket merge levels (as MsmPlan::build + MsmEngine::run)
   const int levels = msm_merge_levels(std::max<uint32_t>(n, 1), prm);
   std::vector<uint32_t> part1(part.size()), hcnt(nb + 1), hoff(nb + 1);

@@ -138,6 +138,7 @@ class MsmPlan {
   const uint32_t* bstart() const { return bstart_; }
   const uint32_t* bend() const { return bend_; }
   const uint32_t* task_off() const { return off_task_; }
+  const uint32_t* perm() const { return use_perm_ ? perm_ : nullptr; }  // task order (by length)
   const uint32_t* level_off(int lv) const { return off_lvl_[lv]; }
   size_t max_tasks_now() const { return max_tasks_now_; }
   size_t max_tasks() const { return max_tasks_; }
@@ -173,6 +174,9 @@ class MsmPlan {
   uint32_t *hs_hist_ = nullptr, *hs_blkoff_ = nullptr, *hs_bintot_ = nullptr, *hs_binbase_ = nullptr;
   uint32_t *hs_toff_ = nullptr, *hs_hist2_ = nullptr, *hs_off2_ = nullptr, *hs_subbase_ = nullptr;
   void *hs_ent_a_ = nullptr, *hs_ent_b_ = nullptr;  // 8-byte (key, base|sign) entries
+  // accumulate-task order by length (ZKP_TASK_ORDER=bucket: bucket order)
+  bool use_perm_ = false;
+  uint32_t *perm_ = nullptr, *tl_hist_ = nullptr, *tl_off_ = nullptr;
   uint32_t* tsum_ = nullptr;                    // tile sums of the look-back-free scans
   size_t tsum_len_ = 0;
   void* sort_tmp_ = nullptr;

@@ -105,11 +105,23 @@ ZDEV uint32_t seg_search(const uint32_t* __restrict__ off, uint32_t nb, uint32_t
   return lo;
 }
 
+// entries of task t: [s0, s1) of bucket b
+ZDEV uint32_t task_len(uint32_t t, const uint32_t* __restrict__ start, const uint32_t* __restrict__ end,
+                       const uint32_t* __restrict__ off, uint32_t nb, uint32_t S) {
+  const uint32_t b = seg_search(off, nb, t);
+  const uint32_t s0 = start[b] + (t - off[b]) * S;
+  return umin(end[b], s0 + S) - s0;
+}
+
+// thread i runs task perm[i] (tasks ordered by length, longest first: the lanes of a wave run
+// equally long chains) or task i (perm == nullptr)
 template <class F>
-ZDEV void accumulate(uint32_t t, const uint32_t* __restrict__ points, const uint32_t* __restrict__ vals,
+ZDEV void accumulate(uint32_t i, const uint32_t* __restrict__ points, const uint32_t* __restrict__ vals,
                      const uint32_t* __restrict__ start, const uint32_t* __restrict__ end,
-                     const uint32_t* __restrict__ off, uint32_t nb, uint32_t S, uint32_t* __restrict__ out) {
-  if (t >= off[nb]) return;
+                     const uint32_t* __restrict__ off, uint32_t nb, uint32_t S, const uint32_t* __restrict__ perm,
+                     uint32_t* __restrict__ out) {
+  if (i >= off[nb]) return;
+  const uint32_t t = perm ? perm[i] : i;
   const uint32_t b = seg_search(off, nb, t);
   const uint32_t s0 = start[b] + (t - off[b]) * S;
   const uint32_t s1 = umin(end[b], s0 + S);
