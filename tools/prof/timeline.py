@@ -14,9 +14,9 @@ def main(path, idx=2):
     rows = [(int(r["Start_Timestamp"]) - t0, int(r["End_Timestamp"]) - t0, short(r["Kernel_Name"]))
             for r in tr if t0 <= int(r["Start_Timestamp"]) < t1]
     for s, e, k in rows:
-        if e - s > 200000 or k.startswith(("k_dsort", "k_scan_", "k_bounds", "k_heavy", "k_task")):
+        if e - s > 200000 or k.startswith(("k_hs_", "k_tlen", "k_lvl", "k_scan_", "k_bounds", "k_heavy", "k_task", "k_join")):
             print("%8.2f %8.2f %7.2f %s" % (s / 1e6, e / 1e6, (e - s) / 1e6, k))
-    sat = [(s, e) for s, e, k in rows if k.startswith(("k_acc", "k_ntt", "rocprim")) and e - s > 100000]
+    sat = [(s, e) for s, e, k in rows if k.startswith(("k_acc", "k_ntt", "rocprim", "k_hs_")) and e - s > 100000]
     ev = sorted([(s, 1) for s, e in sat] + [(e, -1) for s, e in sat])
     cur = last = cov = 0
     for t, d in ev:
