@@ -90,6 +90,33 @@ def main(n=300):
         checks.append(("x8_lsub8_sqr", lambda v, x=x, d=d: v % P == (d - x) ** 2 * inv_rp_p % P and v < 2 * P))
         checks.append(("x8_mul2", lambda v, x=x, a=a, b=b, d=d: v % P == (d * (d - x) - a * b) * inv_rp_p % P
                        and v < 2 * P))
+    # lazily reduced G2 accumulator forms (field.hpp sqr_lazy / sub_2x4, curve.hpp acc_y3):
+    # inputs at the top of their bounds where 8 words can hold them (6m > 2^256: < 2^256 tested)
+    TOP = (1 << 256) - 1
+    def f2sq(a0, a1):
+        return a0 * a0 - a1 * a1, 2 * a0 * a1
+    sq = [[rnd.randrange(TOP), rnd.randrange(TOP)] for _ in range(n)] + [[TOP, TOP], [0, TOP], [TOP, 0], [0, 0]]
+    for a0, a1 in sq:
+        lines.append("sqrlazyf2 %s %s" % (w8(a0), w8(a1)))
+        e = f2sq(a0, a1)
+        for k in range(2):
+            checks.append(("sqrlazyf2", lambda v, x=e[k]: v % P == x * inv_rp_p % P and v < 2 * P))
+    for a, b, c in triples:
+        t = [(a, b), (b, c), (c, a)]
+        lines.append("sub2x4f2 %s" % " ".join(w8(x) for pr in t for x in pr))
+        for k in range(2):
+            x = t[0][k] - t[1][k] - 2 * t[2][k]
+            checks.append(("sub2x4f2", lambda v, x=x: v % P == x % P and v < 4 * P))
+    y3 = [[rnd.randrange(TOP), rnd.randrange(TOP), rnd.randrange(4 * P), rnd.randrange(4 * P),
+           rnd.randrange(2 * P + 1), rnd.randrange(2 * P + 1), rnd.randrange(2 * P), rnd.randrange(2 * P)]
+          for _ in range(n)]
+    y3 += [[TOP, TOP, 4 * P - 1, 4 * P - 1, 2 * P, 2 * P, 2 * P - 1, 2 * P - 1], [0] * 8]
+    for t0, t1, r0, r1, d0, d1, y0, y1 in y3:
+        lines.append("y3f2 %s" % " ".join(w8(x) for x in (t0, t1, r0, r1, d0, d1, y0, y1)))
+        c0 = t0 * r0 - t1 * r1 + d0 * y0 - d1 * y1
+        c1 = t0 * r1 + t1 * r0 + d0 * y1 + d1 * y0
+        for x in (c0, c1):
+            checks.append(("y3f2", lambda v, x=x: v % P == x * inv_rp_p % P and v < 2 * P))
     for z in (0, P):
         lines.append("iszq %s" % w8(z)); checks.append(("iszq", lambda v: v == 1))
     out = subprocess.run([BIN], input="\n".join(lines) + "\n", capture_output=True, text=True).stdout.strip().split("\n")

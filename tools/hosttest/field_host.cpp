@@ -46,6 +46,19 @@ int main() {
       prf(canon8(x)); printf("\n"); prf(mul(x, d)); printf("\n"); prf(sqr(lsub8(d, x))); printf("\n");
       prf(mul2(d, lsub8(d, x), a, rsub(fe_zero<FqCfg>(), b)));
     }
+    else if (o == "sqrlazyf2") {  // G2 lazy square, components < 6m (tested < 2^256)
+      Fq2 a{rdf<FqCfg>(), rdf<FqCfg>()};
+      Fq2 r = sqr_lazy(a); prf(r.c0); printf("\n"); prf(r.c1);
+    }
+    else if (o == "sub2x4f2") {  // G2 lazy X3 (< 4m per component)
+      Fq2 a{rdf<FqCfg>(), rdf<FqCfg>()}, b{rdf<FqCfg>(), rdf<FqCfg>()}, c{rdf<FqCfg>(), rdf<FqCfg>()};
+      Fq2 r = sub_2x4(a, b, c); prf(r.c0); printf("\n"); prf(r.c1);
+    }
+    else if (o == "y3f2") {  // G2 Y3 sum of products t r + d y with t < 6m, r < 4m, d <= 2m, y < 2m
+      Fq2 t{rdf<FqCfg>(), rdf<FqCfg>()}, r{rdf<FqCfg>(), rdf<FqCfg>()}, d{rdf<FqCfg>(), rdf<FqCfg>()},
+          y{rdf<FqCfg>(), rdf<FqCfg>()};
+      Fq2 v = acc_y3(r, t, y, d); prf(v.c0); printf("\n"); prf(v.c1);
+    }
     else if (o == "mulr") { Fr a = rdf<FrCfg>(), b = rdf<FrCfg>(); prf(mul(a, b)); }
     else if (o == "canonq") { Fq a = rdf<FqCfg>(); prf(canon(a)); }
     else if (o == "iszq") { Fq a = rdf<FqCfg>(); printf("%d", (int)is_zero(a)); }

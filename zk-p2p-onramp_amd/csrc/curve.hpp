@@ -39,18 +39,29 @@ ZDEV Fq f_one<Fq>() { return fe_one<FqCfg>(); }
 template <>
 ZDEV Fq2 f_one<Fq2>() { return Fq2{fe_one<FqCfg>(), fe_zero<FqCfg>()}; }
 
-// Accumulator-coordinate forms.  G1: the accumulator x is lazily reduced, < 8m (field.hpp
-// sub_2x8), and the d = 4m - PPP operand of the Y3 sum of products stays unnormalised (rsub:
-// one mul2 operand may have limbs < 2^31, its partner normalised).  G2 keeps canonical
-// coordinates: its Fq2 products need components < 4m.
+// Accumulator-coordinate forms: the XYZZ additions keep x and the differences lazily reduced.
+//  G1: x < 8m (field.hpp sub_2x8: no conditional subtraction), differences with x via lsub8
+//      (< 10m), the d = 4m - PPP operand of the Y3 sum of products unnormalised (rsub: one
+//      mul2 operand may have limbs < 2^31, its partner normalised).
+//  G2: x < 4m (one conditional subtraction per component instead of two), P, R < 6m / 4m
+//      without conditional subtractions, squares of such values by sqr_lazy; the Y3 sum of
+//      products puts the < 6m factor first (Fq2 mul2 negates the SECOND factor's c1, which must
+//      stay <= 4m).  Bounds: field.hpp, host-tested (tools/hosttest).
 ZDEV Fq acc_x3(const Fq& rr, const Fq& ppp, const Fq& q) { return sub_2x8(rr, ppp, q); }
-ZDEV Fq2 acc_x3(const Fq2& rr, const Fq2& ppp, const Fq2& q) { return sub_2x(rr, ppp, q); }
+ZDEV Fq2 acc_x3(const Fq2& rr, const Fq2& ppp, const Fq2& q) { return sub_2x4(rr, ppp, q); }
 ZDEV Fq acc_xsub(const Fq& a, const Fq& x) { return lsub8(a, x); }  // a - x for an accumulator x
-ZDEV Fq2 acc_xsub(const Fq2& a, const Fq2& x) { return lsub(a, x); }
+ZDEV Fq2 acc_xsub(const Fq2& a, const Fq2& x) { return lsub4_lazy(a, x); }
+ZDEV Fq acc_sub(const Fq& a, const Fq& b) { return lsub(a, b); }  // a - b, both < 2m
+ZDEV Fq2 acc_sub(const Fq2& a, const Fq2& b) { return lsub2_lazy(a, b); }
+ZDEV Fq acc_sqr(const Fq& a) { return sqr(a); }  // a < 11m
+ZDEV Fq2 acc_sqr(const Fq2& a) { return sqr_lazy(a); }  // components < 6m
 ZDEV Fq acc_negd(const Fq& a) { return rsub(fe_zero<FqCfg>(), a); }
-ZDEV Fq2 acc_negd(const Fq2& a) { return lsub(Fq2{fe_zero<FqCfg>(), fe_zero<FqCfg>()}, a); }
+ZDEV Fq2 acc_negd(const Fq2& a) { return lsub2_lazy(Fq2{fe_zero<FqCfg>(), fe_zero<FqCfg>()}, a); }
+// Y3 = R T + Y D (T = Q - X3, D = -PPP)
+ZDEV Fq acc_y3(const Fq& r, const Fq& t, const Fq& y, const Fq& d) { return mul2(r, t, y, d); }
+ZDEV Fq2 acc_y3(const Fq2& r, const Fq2& t, const Fq2& y, const Fq2& d) { return mul2(t, r, d, y); }
 ZDEV Fq acc_xcanon(const Fq& x) { return canon8(x); }
-ZDEV Fq2 acc_xcanon(const Fq2& x) { return x; }
+ZDEV Fq2 acc_xcanon(const Fq2& x) { return canon4(x); }
 
 template <class F>
 ZDEV Xyzz<F> xyzz_inf() {
@@ -93,10 +104,13 @@ ZDEV Xyzz<F> xyzz_dbl_aff(const Aff<F>& p) {
   return r;
 }
 
-// 2 * P (dbl-2008-s-1, a = 0)
+// 2 * P (dbl-2008-s-1, a = 0); p.x may be a lazily reduced accumulator x (acc_xcanon first:
+// the doubling formulas take canonical coordinates)
 template <class F>
-ZDEV Xyzz<F> xyzz_dbl(const Xyzz<F>& p) {
-  if (xyzz_is_inf(p)) return p;
+ZDEV Xyzz<F> xyzz_dbl(const Xyzz<F>& p_in) {
+  if (xyzz_is_inf(p_in)) return p_in;
+  Xyzz<F> p = p_in;
+  p.x = acc_xcanon(p.x);
   F U = dbl(p.y);
   F V = sqr(U);
   F W = mul(U, V);
@@ -128,9 +142,9 @@ ZDEV void xyzz_add_aff(Xyzz<F>& acc, const Aff<F>& q, bool neg = false) {
   F U2 = mul(q.x, acc.zz);
   F S2 = mul(qy, acc.zzz);
   F P = acc_xsub(U2, acc.x);
-  F R = lsub(S2, acc.y);
-  F PP = sqr(P);
-  F RR = sqr(R);
+  F R = acc_sub(S2, acc.y);
+  F PP = acc_sqr(P);
+  F RR = acc_sqr(R);
   if (is_zero(PP)) {
     if (is_zero(RR)) {
       Aff<F> qs = q;
@@ -144,7 +158,7 @@ ZDEV void xyzz_add_aff(Xyzz<F>& acc, const Aff<F>& q, bool neg = false) {
   F PPP = mul(P, PP);
   F Q = mul(acc.x, PP);
   F X3 = acc_x3(RR, PPP, Q);
-  F Y3 = mul2(R, acc_xsub(Q, X3), acc.y, acc_negd(PPP));  // R (Q - X3) - Y1 PPP
+  F Y3 = acc_y3(R, acc_xsub(Q, X3), acc.y, acc_negd(PPP));  // R (Q - X3) - Y1 PPP
   acc.zz = mul(acc.zz, PP);
   acc.zzz = mul(acc.zzz, PPP);
   acc.x = X3;
@@ -164,10 +178,10 @@ ZDEV Xyzz<F> xyzz_from_aff_pair(const Aff<F>& p, bool np, const Aff<F>& q, bool 
   }
   const F py = np ? sub(f_zero<F>(), p.y) : p.y;
   const F qy = nq ? sub(f_zero<F>(), q.y) : q.y;
-  F P = lsub(q.x, p.x);
-  F R = lsub(qy, py);
-  F PP = sqr(P);
-  F RR = sqr(R);
+  F P = acc_sub(q.x, p.x);
+  F R = acc_sub(qy, py);
+  F PP = acc_sqr(P);
+  F RR = acc_sqr(R);
   if (is_zero(PP)) {
     if (is_zero(RR)) return xyzz_dbl_aff(Aff<F>{p.x, py});
     return acc;  // p == -q
@@ -175,7 +189,7 @@ ZDEV Xyzz<F> xyzz_from_aff_pair(const Aff<F>& p, bool np, const Aff<F>& q, bool 
   F PPP = mul(P, PP);
   F Q = mul(p.x, PP);
   acc.x = acc_x3(RR, PPP, Q);
-  acc.y = mul2(R, acc_xsub(Q, acc.x), py, acc_negd(PPP));  // R (Q - X3) - Y1 PPP
+  acc.y = acc_y3(R, acc_xsub(Q, acc.x), py, acc_negd(PPP));  // R (Q - X3) - Y1 PPP
   acc.zz = PP;
   acc.zzz = PPP;
   return acc;
@@ -193,10 +207,10 @@ ZDEV void xyzz_add(Xyzz<F>& acc, const Xyzz<F>& q) {
   F U2 = mul(q.x, acc.zz);
   F S1 = mul(acc.y, q.zzz);
   F S2 = mul(q.y, acc.zzz);
-  F P = lsub(U2, U1);
-  F R = lsub(S2, S1);
-  F PP = sqr(P);
-  F RR = sqr(R);
+  F P = acc_sub(U2, U1);
+  F R = acc_sub(S2, S1);
+  F PP = acc_sqr(P);
+  F RR = acc_sqr(R);
   if (is_zero(PP)) {
     if (is_zero(RR))
       acc = xyzz_dbl(acc);
@@ -207,7 +221,7 @@ ZDEV void xyzz_add(Xyzz<F>& acc, const Xyzz<F>& q) {
   F PPP = mul(P, PP);
   F Q = mul(U1, PP);
   F X3 = acc_x3(RR, PPP, Q);
-  F Y3 = mul2(R, acc_xsub(Q, X3), S1, acc_negd(PPP));  // R (Q - X3) - S1 PPP
+  F Y3 = acc_y3(R, acc_xsub(Q, X3), S1, acc_negd(PPP));  // R (Q - X3) - S1 PPP
   acc.zz = mul(mul(acc.zz, q.zz), PP);
   acc.zzz = mul(mul(acc.zzz, q.zzz), PPP);
   acc.x = X3;

@@ -323,6 +323,32 @@ ZDEV Fe<C> lsub8(const Fe<C>& a, const Fe<C>& b) {
 template <class C>
 ZDEV Fe<C> canon8(const Fe<C>& a) { return cond_sub(cond_sub(a, C::MOD4), C::MOD2); }
 
+// a - b + 4m (b < 4m) and a - b + 6m (b < 6m), normalised: mul / sqr operands
+template <class C>
+ZDEV Fe<C> lsub4(const Fe<C>& a, const Fe<C>& b) {
+  Fe<C> s;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) s.v[i] = a.v[i] + C::MOD4_BORROW[i] - b.v[i];
+  normalize(s);
+  return s;
+}
+template <class C>
+ZDEV Fe<C> lsub6(const Fe<C>& a, const Fe<C>& b) {
+  Fe<C> s;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) s.v[i] = a.v[i] + C::MOD6_BORROW[i] - b.v[i];
+  normalize(s);
+  return s;
+}
+// 2a, limbs shifted (raw: limbs < 2^30 for a normalised a): ONE operand of mul()
+template <class C>
+ZDEV Fe<C> shl1_raw(const Fe<C>& a) {
+  Fe<C> s;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) s.v[i] = a.v[i] << 1;
+  return s;
+}
+
 // ---- lazy radix-4 sums (NTT): a first-stage sum x + y of two normalised values < 2m is kept
 // raw (limbs < 2^30, value < 4m, no carry pass and no conditional subtraction); the second
 // stage consumes two such sums:
@@ -503,6 +529,25 @@ ZDEV Fq2 sqr(const Fq2& a) {
   r.c1 = add(t, t);
   return r;
 }
+
+// ---- lazily reduced G2 accumulator forms (curve.hpp acc_*): every component normalised, value
+// bounds as noted; the products stay < 2m as long as each Fq sum of products of a Fq2 mul/mul2
+// (neg4 on the second operand's c1, which must be <= 4m) stays below ~169 m^2.
+// a - b + 2m per component for a, b < 2m: < 4m, no conditional subtraction
+ZDEV Fq2 lsub2_lazy(const Fq2& a, const Fq2& b) { return Fq2{lsub(a.c0, b.c0), lsub(a.c1, b.c1)}; }
+// a - b + 4m per component for a < 2m, b < 4m: < 6m
+ZDEV Fq2 lsub4_lazy(const Fq2& a, const Fq2& b) { return Fq2{lsub4(a.c0, b.c0), lsub4(a.c1, b.c1)}; }
+// a^2 for components < 6m: (a0 + a1)(a0 - a1 + 6m) [raw sum x normalised, < 144 m^2] and
+// (2 a0) a1 [raw x normalised, < 72 m^2] -- no additions reduced, no doubling of the product
+ZDEV Fq2 sqr_lazy(const Fq2& a) {
+  return Fq2{mul(add_raw(a.c0, a.c1), lsub6(a.c0, a.c1)), mul(shl1_raw(a.c0), a.c1)};
+}
+// R^2 - PPP - 2Q per component (each < 2m) -> < 4m: one conditional subtraction instead of two
+ZDEV Fq2 sub_2x4(const Fq2& a, const Fq2& b, const Fq2& c) {
+  return Fq2{cond_sub(sub_2x8(a.c0, b.c0, c.c0), FqCfg::MOD4), cond_sub(sub_2x8(a.c1, b.c1, c.c1), FqCfg::MOD4)};
+}
+// components < 4m -> < 2m
+ZDEV Fq2 canon4(const Fq2& a) { return Fq2{cond_sub(a.c0, FqCfg::MOD2), cond_sub(a.c1, FqCfg::MOD2)}; }
 
 ZDEV Fq2 add(const Fq2& a, const Fq2& b) { return Fq2{add(a.c0, b.c0), add(a.c1, b.c1)}; }
 // Fq2 lazy forms: Karatsuba mul() adds the components of each operand, so a raw
