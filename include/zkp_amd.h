@@ -93,6 +93,15 @@ void zkp_buffer_free(uint8_t* p);
 zkp_status zkp_zkey_contribute(int device, const uint8_t* zkey, size_t len, const uint8_t* k32, uint8_t** out,
                                size_t* out_len);
 
+/* Setup acceleration: `snarkjs zkey new <circuit.r1cs> <pot.ptau> <circuit_0000.zkey>`
+ * (reference dizkus-scripts/3_gen_chunk_zkey.sh:18) on `device`: the phase-2 starting key
+ * (gamma = delta = 1) of a circom .r1cs (v1) from a prepared .ptau (v1, Lagrange sections 12-15,
+ * power >= log2(domain) + 1).  A/B1/B2/IC/L are sparse sums of ptau Lagrange points with the
+ * circuit's coefficients, built on the GPU; H is copied from the odd points of the next level.
+ * Section 10 holds no contributions and a zero csHash.  *out: the zkey (zkp_buffer_free). */
+zkp_status zkp_zkey_new(int device, const uint8_t* r1cs, size_t r1cs_len, const uint8_t* ptau, size_t ptau_len,
+                        uint8_t** out, size_t* out_len);
+
 /* Load only point slice `part` of `nparts` (contiguous ranges of the witness-indexed
  * sections 5-8 and of section 9) onto one device.  Such a prover computes partial sums
  * only (zkp_prove_partial); the quotient is computed in full on every part. */

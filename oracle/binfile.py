@@ -67,6 +67,47 @@ def read_wtns(buf: bytes):
     return q, w
 
 
+# ------------------------------------------------------------------ r1cs / ptau (setup inputs)
+
+
+def write_r1cs(r1cs) -> bytes:
+    """circom ``.r1cs`` v1 (binfile "r1cs"; read by snarkjs ``zkey new`` through the r1csfile
+    package, reference call site dizkus-scripts/3_gen_chunk_zkey.sh:18; recalled layout,
+    unpinned offline): section 1 header (u32 n8, prime r, u32 nWires, u32 nPubOut, u32 nPubIn,
+    u32 nPrvIn, u64 nLabels, u32 nConstraints), section 2 the constraints (A, B, C linear
+    combinations: u32 count, then count x (u32 wire, n8-byte LE coefficient)), section 3 the
+    wire -> label map (u64 per wire).  All public signals are written as public inputs."""
+    n8 = 32
+    npub = r1cs.n_public
+    sec1 = (struct.pack("<I", n8) + bn254.int_to_le(bn254.R) +
+            struct.pack("<IIII", r1cs.n_vars, 0, npub, r1cs.n_vars - 1 - npub) +
+            struct.pack("<QI", r1cs.n_vars, r1cs.n_constraints))
+    parts = []
+    for lcs in r1cs.constraints:
+        for lc in lcs:
+            parts.append(struct.pack("<I", len(lc)))
+            for sig, v in lc:
+                parts.append(struct.pack("<I", sig) + bn254.int_to_le(v % bn254.R))
+    sec3 = b"".join(struct.pack("<Q", i) for i in range(r1cs.n_vars))
+    return write_binfile(b"r1cs", 1, [(1, sec1), (2, b"".join(parts)), (3, sec3)])
+
+
+def write_ptau(power: int, tau_g1, tau_g2, alpha_tau_g1, beta_tau_g1, beta_g2, l_tau_g1, l_tau_g2,
+               l_alpha_tau_g1, l_beta_tau_g1) -> bytes:
+    """snarkjs ``.ptau`` v1 after ``powersoftau prepare phase2`` (recalled layout, unpinned
+    offline): 1 header (u32 n8, prime q, u32 power, u32 ceremonyPower), 2 tauG1 (2^(power+1)-1
+    points), 3 tauG2 (2^power), 4 alphaTauG1, 5 betaTauG1 (2^power each), 6 betaG2, 7 the
+    contributions (u32 count = 0), 12..15 the Lagrange forms lTauG1, lTauG2, lAlphaTauG1,
+    lBetaTauG1 of every level p = 0..power concatenated (level p = 2^p points at 2^p - 1)."""
+    g1 = lambda pts: b"".join(bn254.g1_to_lem(p) for p in pts)
+    g2 = lambda pts: b"".join(bn254.g2_to_lem(p) for p in pts)
+    sec1 = struct.pack("<I", 32) + bn254.int_to_le(bn254.P) + struct.pack("<II", power, power)
+    return write_binfile(b"ptau", 1, [
+        (1, sec1), (2, g1(tau_g1)), (3, g2(tau_g2)), (4, g1(alpha_tau_g1)), (5, g1(beta_tau_g1)),
+        (6, g2([beta_g2])), (7, struct.pack("<I", 0)),
+        (12, g1(l_tau_g1)), (13, g2(l_tau_g2)), (14, g1(l_alpha_tau_g1)), (15, g1(l_beta_tau_g1))])
+
+
 # ------------------------------------------------------------------ zkey
 
 

@@ -109,7 +109,10 @@ def zkey_coefs(r1cs: R1CS):
 
 
 def setup(r1cs: R1CS, seed: int) -> ZKey:
-    tw = toxic_from_seed(seed)
+    return setup_toxic(r1cs, toxic_from_seed(seed))
+
+
+def setup_toxic(r1cs: R1CS, tw: dict) -> ZKey:
     tau, alpha, beta, gamma, delta = tw["tau"], tw["alpha"], tw["beta"], tw["gamma"], tw["delta"]
     n = domain_size_for(r1cs.n_constraints, r1cs.n_public)
     A, B, C = qap_at_tau(r1cs, tau, n)
@@ -173,3 +176,38 @@ def contribute_delta(z: ZKey, k: int) -> ZKey:
     out.c = [None if p is None else bn254.g1_mul(p, ki) for p in z.c]
     out.h = [None if p is None else bn254.g1_mul(p, ki) for p in z.h]
     return out
+
+
+# ------------------------------------------------------------------ `zkey new` from a ptau
+
+
+def zkey_new(r1cs: R1CS, tau: int, alpha: int, beta: int) -> ZKey:
+    """What ``snarkjs zkey new <r1cs> <ptau>`` produces (reference dizkus-scripts/
+    3_gen_chunk_zkey.sh:18) from a ptau of toxic waste (tau, alpha, beta): the phase-2 key
+    before any contribution, gamma = delta = 1 (the generators).  Equal to the known-tau setup
+    with those values, which is how the GPU builder (zkp_zkey_new) is checked."""
+    return setup_toxic(r1cs, dict(tau=tau, alpha=alpha, beta=beta, gamma=1, delta=1))
+
+
+def ptau_known_tau(power: int, tau: int, alpha: int, beta: int) -> bytes:
+    """An INSECURE ptau of known toxic waste (tau, alpha, beta), binfile.write_ptau layout."""
+    from .binfile import write_ptau
+    g1 = bn254.FixedBase(bn254.G1_GEN)
+    g2 = bn254.FixedBase(bn254.G2_GEN, g2=True)
+    N = 1 << power
+    pw = [1]
+    for _ in range(2 * N - 2):
+        pw.append(pw[-1] * tau % R)
+    tau_g1 = bn254.batch_to_affine_g1([g1.mul_jac(x) for x in pw])
+    tau_g2 = [g2.mul(x) for x in pw[:N]]
+    alpha_tau = bn254.batch_to_affine_g1([g1.mul_jac(alpha * x % R) for x in pw[:N]])
+    beta_tau = bn254.batch_to_affine_g1([g1.mul_jac(beta * x % R) for x in pw[:N]])
+    lag = []
+    for p in range(power + 1):
+        lag += lagrange_at(tau, 1 << p, ROOTS[p])
+    l_tau_g1 = bn254.batch_to_affine_g1([g1.mul_jac(x) for x in lag])
+    l_tau_g2 = [g2.mul(x) for x in lag]
+    l_alpha = bn254.batch_to_affine_g1([g1.mul_jac(alpha * x % R) for x in lag])
+    l_beta = bn254.batch_to_affine_g1([g1.mul_jac(beta * x % R) for x in lag])
+    return write_ptau(power, tau_g1, tau_g2, alpha_tau, beta_tau, g2.mul(beta), l_tau_g1, l_tau_g2, l_alpha,
+                      l_beta)

@@ -201,6 +201,14 @@ zkp_status zkp_zkey_contribute(int device, const uint8_t* zkey, size_t len, cons
   return s != ZKP_OK ? s : hand_out(std::move(buf), out, out_len);
 }
 
+zkp_status zkp_zkey_new(int device, const uint8_t* r1cs, size_t r1cs_len, const uint8_t* ptau, size_t ptau_len,
+                        uint8_t** out, size_t* out_len) {
+  if (!r1cs || !ptau || !out || !out_len) return fail(ZKP_ERR_INVALID_ARG, "null argument");
+  std::vector<uint8_t> buf;
+  zkp_status s = guard([&] { buf = zkp::zkey_new(device, r1cs, r1cs_len, ptau, ptau_len); });
+  return s != ZKP_OK ? s : hand_out(std::move(buf), out, out_len);
+}
+
 zkp_status zkp_prover_load_part(const uint8_t* zkey, size_t len, int device, int part, int nparts,
                                 zkp_prover** out) {
   if (!zkey || !out) return fail(ZKP_ERR_INVALID_ARG, "null argument");

@@ -114,6 +114,9 @@ void proof_combine(const uint8_t* zkey, size_t len, const zkp_partial* parts, in
 
 // phase-2 contribution math on the GPU (setup.hip): delta -> k*delta
 std::vector<uint8_t> zkey_apply_delta(int device, const uint8_t* zkey, size_t len, const uint8_t* k32);
+// `snarkjs zkey new`: the phase-2 starting key (gamma = delta = 1) of a circom .r1cs from a
+// prepared .ptau (sections 12-15), the point sections built on `device` (zkey_new.hip)
+std::vector<uint8_t> zkey_new(int device, const uint8_t* r1cs, size_t r1cs_len, const uint8_t* ptau, size_t ptau_len);
 
 // kernel-level helpers (C-ABI zkp_msm_g1/g2, zkp_ntt_fr)
 // c / depth: window bits and base-table depth (0 = automatic, as the prover)

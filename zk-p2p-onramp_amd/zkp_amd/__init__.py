@@ -116,6 +116,7 @@ def load_library(path: str = LIB_PATH):
         lib.zkp_zkey_read_chunks.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.c_int, ctypes.POINTER(u8p),
                                              ctypes.POINTER(sz)]
         lib.zkp_zkey_contribute.argtypes = [ctypes.c_int, u8p, sz, u8p, ctypes.POINTER(u8p), ctypes.POINTER(sz)]
+        lib.zkp_zkey_new.argtypes = [ctypes.c_int, u8p, sz, u8p, sz, ctypes.POINTER(u8p), ctypes.POINTER(sz)]
         lib.zkp_buffer_free.argtypes = [u8p]
         lib.zkp_buffer_free.restype = None
         lib.zkp_prover_load_part.argtypes = [u8p, sz, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(P)]
@@ -131,7 +132,7 @@ def load_library(path: str = LIB_PATH):
                      "zkp_witness_stage", "zkp_prove_staged", "zkp_prover_instrument", "zkp_prover_kernel_stats",
                      "zkp_bench_msm", "zkp_bench_ntt", "zkp_bench_plan", "zkp_msm", "zkp_prover_msm_config",
                      "zkp_prover_load_part", "zkp_prove_partial", "zkp_proof_calldata",
-                     "zkp_prover_load_chunks", "zkp_zkey_read", "zkp_zkey_read_chunks", "zkp_zkey_contribute", "zkp_prove_partial_staged", "zkp_proof_combine",
+                     "zkp_prover_load_chunks", "zkp_zkey_read", "zkp_zkey_read_chunks", "zkp_zkey_contribute", "zkp_zkey_new", "zkp_prove_partial_staged", "zkp_proof_combine",
                      "zkp_quotient_part_staged", "zkp_prove_partial_ext_staged"):
             getattr(lib, name).restype = ctypes.c_int
         _lib = lib
@@ -488,6 +489,21 @@ def zkey_contribute(zkey: bytes, k: int, device: int = 0) -> bytes:
     out = ctypes.POINTER(ctypes.c_uint8)()
     n = ctypes.c_size_t()
     _check(lib.zkp_zkey_contribute(device, zp, zlen, kp, ctypes.byref(out), ctypes.byref(n)))
+    try:
+        return _copy_out(out, n.value)
+    finally:
+        lib.zkp_buffer_free(out)
+
+
+def zkey_new(r1cs: bytes, ptau: bytes, device: int = 0) -> bytes:
+    """`snarkjs zkey new`: the phase-2 starting key of a circom .r1cs from a prepared .ptau,
+    point sections built on the GPU (zkp_zkey_new)."""
+    lib = load_library()
+    rp, rk = _buf(r1cs)
+    pp, pk = _buf(ptau)
+    out = ctypes.POINTER(ctypes.c_uint8)()
+    n = ctypes.c_size_t()
+    _check(lib.zkp_zkey_new(device, rp, len(r1cs), pp, len(ptau), ctypes.byref(out), ctypes.byref(n)))
     try:
         return _copy_out(out, n.value)
     finally:
