@@ -105,3 +105,35 @@ def test_node_mem_zkey_resident_and_release_while_in_flight():
     assert r.returncode == 0, r.stdout + r.stderr
     out = json.loads(r.stdout.strip().splitlines()[-1])
     assert out["same"] and out["proof"] == json.load(open(os.path.join(GOLD, "proof_small.json")))
+
+
+def test_addon_zkey_new_checks_arguments():
+    r = node("const a=require('./zk-p2p-onramp_amd/js/build/zkp_napi.node');"
+             "const z=require('./zk-p2p-onramp_amd/js/groth16.js');"
+             "let out=[typeof a.zkeyNew, typeof z.zKey.newZKey];"
+             "try{a.zkeyNew('x')}catch(e){out.push(e.message)}"
+             "console.log(JSON.stringify(out))")
+    assert r.returncode == 0, r.stderr
+    t1, t2, msg = json.loads(r.stdout.strip().splitlines()[-1])
+    assert t1 == t2 == "function" and "zkeyNew(r1csBuffer, ptauBuffer" in msg
+
+
+@pytest.mark.gpu
+def test_node_cli_zkey_new(tmp_path):
+    """`cli.js zkey new|groth16 setup <r1cs> <ptau> <zkey>` (snarkjs' setup step, reference
+    dizkus-scripts/3_gen_chunk_zkey.sh:18) writes the oracle's key byte for byte."""
+    from oracle import binfile, circuit, groth16, setup
+    TAU, ALPHA, BETA = 0x1234567890ABCDEF1122334455667788 % groth16.R, 987654321987654321, 555555555555
+    m = json.load(open(os.path.join(GOLD, "manifest.json")))["circuits"]["tiny"]
+    r1cs, _ = circuit.gen_circuit(m["n_vars"], m["n_constraints"], m["n_public"], m["circuit_seed"])
+    k = circuit.domain_size_for(r1cs.n_constraints, r1cs.n_public).bit_length() - 1
+    (tmp_path / "c.r1cs").write_bytes(binfile.write_r1cs(r1cs))
+    (tmp_path / "p.ptau").write_bytes(setup.ptau_known_tau(k + 1, TAU, ALPHA, BETA))
+    want = binfile.write_zkey(setup.zkey_new(r1cs, TAU, ALPHA, BETA))
+    for i, argv in enumerate([["zkey", "new"], ["groth16", "setup"]]):  # the reference runs `groth16 setup ... -e=`
+        out = tmp_path / ("c%d.zkey" % i)
+        extra = ["-e=some entropy"] if argv[0] == "groth16" else []
+        r = subprocess.run([NODE, os.path.join(JS, "cli.js")] + argv + [str(tmp_path / "c.r1cs"), str(tmp_path / "p.ptau"),
+                           str(out)] + extra, capture_output=True, text=True, timeout=600)
+        assert r.returncode == 0, r.stderr
+        assert out.read_bytes() == want

@@ -7,18 +7,26 @@
  * Output files are JSON.stringify(x, null, 1), byte-identical in layout to snarkjs.
  * and snarkjs' calldata export (reference circuit/scripts/generate_calldata.sh:3):
  *   node cli.js zkey export soliditycalldata <public.json> <proof.json>
+ * and snarkjs' setup step (reference dizkus-scripts/3_gen_chunk_zkey.sh:18, `groth16 setup`):
+ *   node cli.js groth16 setup|zkey new <circuit.r1cs> <pot.ptau> <circuit_0000.zkey> [-e=...]
  */
 const fs = require('fs');
-const { groth16, exportSolidityCallData, release } = require('./groth16');
+const { groth16, exportSolidityCallData, newZKey, release } = require('./groth16');
 
 const USAGE = 'usage: cli.js groth16 prove <circuit.zkey> <witness.wtns> <proof.json> <public.json>\n' +
-              '       cli.js zkey export soliditycalldata <public.json> <proof.json>\n';
+              '       cli.js zkey export soliditycalldata <public.json> <proof.json>\n' +
+              '       cli.js groth16 setup|zkey new <circuit.r1cs> <pot.ptau> <circuit_0000.zkey>\n';
 
 async function main(argv) {
   if (argv.length === 5 && argv[0] === 'zkey' && argv[1] === 'export' && argv[2] === 'soliditycalldata') {
     const pub = JSON.parse(fs.readFileSync(argv[3], 'utf-8'));
     const proof = JSON.parse(fs.readFileSync(argv[4], 'utf-8'));
     process.stdout.write(await exportSolidityCallData(proof, pub) + '\n');
+    return 0;
+  }
+  const setupArgs = argv.filter((a) => !a.startsWith('-e='));  // entropy: unused by `groth16 setup`
+  if (setupArgs.length === 5 && ((argv[0] === 'zkey' && argv[1] === 'new') || (argv[0] === 'groth16' && argv[1] === 'setup'))) {
+    await newZKey(setupArgs[2], setupArgs[3], setupArgs[4]);
     return 0;
   }
   if (argv.length !== 6 || argv[0] !== 'groth16' || argv[1] !== 'prove') {

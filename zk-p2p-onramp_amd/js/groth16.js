@@ -135,6 +135,20 @@ function onRampArgs(proof, publicSignals) {
   ];
 }
 
+/*
+ * snarkjs' `zKey.newZKey(r1csName, ptauName, zkeyName, logger)` (the `zkey new` step,
+ * reference dizkus-scripts/3_gen_chunk_zkey.sh:18): the phase-2 initial key (gamma = delta = 1)
+ * built on the GPU.  r1cs / ptau are paths or {type:"mem"} descriptors; with a zkeyName the key
+ * is written there, and the key bytes are returned either way.
+ */
+async function newZKey(r1csName, ptauName, zkeyName, logger, device) {
+  const out = addon.zkeyNew(readInput(r1csName), readInput(ptauName), device || 0);
+  if (typeof zkeyName === 'string') fs.writeFileSync(zkeyName, out);
+  else if (zkeyName && typeof zkeyName === 'object' && zkeyName.type === 'mem') zkeyName.data = out;
+  if (logger && logger.info) logger.info(`zkey new: ${out.length} bytes`);
+  return out;
+}
+
 function release() {
   for (const h of provers.values()) addon.freeProver(h);
   for (const h of memProvers.values()) addon.freeProver(h);
@@ -145,7 +159,8 @@ function release() {
 module.exports = {
   groth16: { prove, proveBatch },
   proveBatch,
-  zKey: { exportSolidityCallData },
+  zKey: { exportSolidityCallData, newZKey },
+  newZKey,
   prove,
   exportSolidityCallData,
   onRampArgs,

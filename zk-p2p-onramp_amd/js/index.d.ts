@@ -24,6 +24,9 @@ export declare function prove(zkey: Input, wtns: Input, logger?: Logger, opts?: 
   Promise<{ proof: Proof; publicSignals: string[] }>;
 export declare const zKey: {
   exportSolidityCallData(proof: Proof, publicSignals: string[]): Promise<string>;
+  /** `snarkjs zkey new` on the GPU; writes zkeyName when given, returns the key bytes */
+  newZKey(r1csName: Input, ptauName: Input, zkeyName?: string | { type: "mem"; data?: Uint8Array }, logger?: Logger,
+          device?: number): Promise<Buffer>;
 };
 export declare function exportSolidityCallData(proof: Proof, publicSignals: string[]): Promise<string>;
 export declare function onRampArgs(proof: Proof, publicSignals: string[]):

@@ -9,6 +9,7 @@
  *   proveBatch(handle, [wtnsBuffer...], rs?, ss?) -> Promise<[result | Error, ...]> (zkp_prove_batch_status:
  *                                                    every proof attempted, per-proof errors)
  *   freeProver(handle)
+ *   zkeyNew(r1csBuffer, ptauBuffer, device?)     -> Buffer (`snarkjs zkey new`, synchronous)
  *   version()
  * prove()/proveBatch() run on the libuv threadpool (napi_async_work), so the JS main
  * thread is never blocked — the same async contract as snarkjs' Promise API.
@@ -75,6 +76,43 @@ static napi_value js_version(napi_env env, napi_callback_info info) {
   napi_value s;
   NAPI_CALL(env, napi_create_string_utf8(env, zkp_version(), NAPI_AUTO_LENGTH, &s));
   return s;
+}
+
+/* zkeyNew(r1csBuffer, ptauBuffer, device?) -> Buffer: `snarkjs zkey new` (zkp_zkey_new),
+ * synchronous -- a setup step, not a serving path */
+static napi_value js_zkey_new(napi_env env, napi_callback_info info) {
+  size_t argc = 3;
+  napi_value argv[3];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  bool b0 = false, b1 = false;
+  if (argc >= 2) {
+    napi_is_buffer(env, argv[0], &b0);
+    napi_is_buffer(env, argv[1], &b1);
+  }
+  if (!b0 || !b1) {
+    napi_throw_type_error(env, NULL, "zkeyNew(r1csBuffer, ptauBuffer, device?)");
+    return NULL;
+  }
+  int device = 0;
+  if (argc > 2) napi_get_value_int32(env, argv[2], &device);
+  void *r1cs, *ptau;
+  size_t r1cs_len, ptau_len;
+  NAPI_CALL(env, napi_get_buffer_info(env, argv[0], &r1cs, &r1cs_len));
+  NAPI_CALL(env, napi_get_buffer_info(env, argv[1], &ptau, &ptau_len));
+  uint8_t* out = NULL;
+  size_t out_len = 0;
+  zkp_status st = zkp_zkey_new(device, (const uint8_t*)r1cs, r1cs_len, (const uint8_t*)ptau, ptau_len, &out, &out_len);
+  if (st != ZKP_OK) return throw_status(env, st);
+  napi_value buf;
+  void* dst = NULL;
+  napi_status ns = napi_create_buffer(env, out_len, &dst, &buf);
+  if (ns == napi_ok) memcpy(dst, out, out_len);
+  zkp_buffer_free(out);
+  if (ns != napi_ok) {
+    napi_throw_error(env, NULL, "N-API call failed: napi_create_buffer");
+    return NULL;
+  }
+  return buf;
 }
 
 static napi_value js_load(napi_env env, napi_callback_info info) {
@@ -466,6 +504,7 @@ static napi_value init(napi_env env, napi_value exports) {
       {"prove", NULL, js_prove, NULL, NULL, NULL, napi_default, NULL},
       {"proveBatch", NULL, js_prove_batch, NULL, NULL, NULL, napi_default, NULL},
       {"freeProver", NULL, js_free, NULL, NULL, NULL, napi_default, NULL},
+      {"zkeyNew", NULL, js_zkey_new, NULL, NULL, NULL, napi_default, NULL},
   };
   napi_define_properties(env, exports, sizeof props / sizeof props[0], props);
   return exports;
