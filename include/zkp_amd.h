@@ -93,6 +93,15 @@ void zkp_buffer_free(uint8_t* p);
 zkp_status zkp_zkey_contribute(int device, const uint8_t* zkey, size_t len, const uint8_t* k32, uint8_t** out,
                                size_t* out_len);
 
+/* Setup acceleration: `snarkjs zkey beacon <in.zkey> <out.zkey> <beaconHashHex> <numIterationsExp>`
+ * (reference dizkus-scripts/3_gen_chunk_zkey.sh:36).  zkp_beacon_secret (host only) derives the
+ * contribution scalar as snarkjs@0.4.22 / ffjavascript do: 2^e chained SHA-256 of the beacon, a
+ * ChaCha20 stream seeded with the hash, Fr.fromRng; k32: 32-byte LE.  zkp_zkey_beacon applies it
+ * with zkp_zkey_contribute (section 10 unchanged).  e <= 63. */
+zkp_status zkp_beacon_secret(const uint8_t* beacon, size_t len, uint32_t num_iterations_exp, uint8_t* k32);
+zkp_status zkp_zkey_beacon(int device, const uint8_t* zkey, size_t len, const uint8_t* beacon, size_t beacon_len,
+                           uint32_t num_iterations_exp, uint8_t** out, size_t* out_len);
+
 /* Setup acceleration: `snarkjs zkey new <circuit.r1cs> <pot.ptau> <circuit_0000.zkey>`
  * (reference dizkus-scripts/3_gen_chunk_zkey.sh:18) on `device`: the phase-2 starting key
  * (gamma = delta = 1) of a circom .r1cs (v1) from a prepared .ptau (v1, Lagrange sections 12-15,

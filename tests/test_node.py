@@ -137,3 +137,29 @@ def test_node_cli_zkey_new(tmp_path):
                            str(out)] + extra, capture_output=True, text=True, timeout=600)
         assert r.returncode == 0, r.stderr
         assert out.read_bytes() == want
+
+
+def test_node_zkey_beacon_checks_arguments():
+    """snarkjs' argument checks (hex beacon, 10 <= numIterationsExp <= 63) before any GPU work."""
+    r = node("const z=require('./zk-p2p-onramp_amd/js/groth16.js');"
+             "(async()=>{const out=[];"
+             " for (const [h,e] of [['zz',10],['',10],['0102',9],['0102',64]]) {"
+             "  try{await z.zKey.beacon(Buffer.alloc(4), undefined, 'n', h, e); out.push('NO')}catch(x){out.push(x.message)} }"
+             " console.log(JSON.stringify(out))})()")
+    assert r.returncode == 0, r.stderr
+    msgs = json.loads(r.stdout.strip().splitlines()[-1])
+    assert [m.split(".")[0] for m in msgs] == ["Invalid Beacon Hash"] * 2 + ["Invalid numIterationsExp"] * 2
+
+
+@pytest.mark.gpu
+def test_node_cli_zkey_beacon(tmp_path):
+    """`cli.js zkey beacon <in> <out> <hex> 10 -n=...` (reference 3_gen_chunk_zkey.sh:36) writes the
+    oracle's contribution with the beacon's secret (oracle/beacon.py)."""
+    from oracle import beacon, binfile, setup
+    zk = os.path.join(GOLD, "circuit_tiny.zkey")
+    hx = "0102030405060708090a0b0c0d0e0f101112131415161718191a1b1c1d1e1f20"
+    r = subprocess.run([NODE, os.path.join(JS, "cli.js"), "zkey", "beacon", zk, str(tmp_path / "b.zkey"), hx, "10",
+                        "-n=Final Beacon phase2"], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr
+    want = setup.contribute_delta(binfile.read_zkey(open(zk, "rb").read()), beacon.beacon_secret(bytes.fromhex(hx), 10))
+    assert (tmp_path / "b.zkey").read_bytes() == binfile.write_zkey(want)

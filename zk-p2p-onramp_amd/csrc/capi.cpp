@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "../../include/zkp_amd.h"
+#include "beacon.hpp"
 #include "hip_check.hpp"
 #include "host_ec.hpp"
 #include "prover.hpp"
@@ -198,6 +199,23 @@ zkp_status zkp_zkey_contribute(int device, const uint8_t* zkey, size_t len, cons
   if (!zkey || !k32 || !out || !out_len) return fail(ZKP_ERR_INVALID_ARG, "null argument");
   std::vector<uint8_t> buf;
   zkp_status s = guard([&] { buf = zkp::zkey_apply_delta(device, zkey, len, k32); });
+  return s != ZKP_OK ? s : hand_out(std::move(buf), out, out_len);
+}
+
+zkp_status zkp_beacon_secret(const uint8_t* beacon, size_t len, uint32_t num_iterations_exp, uint8_t* k32) {
+  if ((!beacon && len) || !k32) return fail(ZKP_ERR_INVALID_ARG, "null argument");
+  return guard([&] { zkp::beacon_secret(beacon, len, num_iterations_exp, k32); });
+}
+
+zkp_status zkp_zkey_beacon(int device, const uint8_t* zkey, size_t len, const uint8_t* beacon, size_t beacon_len,
+                           uint32_t num_iterations_exp, uint8_t** out, size_t* out_len) {
+  if (!zkey || (!beacon && beacon_len) || !out || !out_len) return fail(ZKP_ERR_INVALID_ARG, "null argument");
+  std::vector<uint8_t> buf;
+  zkp_status s = guard([&] {
+    uint8_t k[32];
+    zkp::beacon_secret(beacon, beacon_len, num_iterations_exp, k);
+    buf = zkp::zkey_apply_delta(device, zkey, len, k);
+  });
   return s != ZKP_OK ? s : hand_out(std::move(buf), out, out_len);
 }
 

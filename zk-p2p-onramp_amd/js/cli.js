@@ -9,13 +9,16 @@
  *   node cli.js zkey export soliditycalldata <public.json> <proof.json>
  * and snarkjs' setup step (reference dizkus-scripts/3_gen_chunk_zkey.sh:18, `groth16 setup`):
  *   node cli.js groth16 setup|zkey new <circuit.r1cs> <pot.ptau> <circuit_0000.zkey> [-e=...]
+ * and the final beacon (3_gen_chunk_zkey.sh:36; no transcript record is appended):
+ *   node cli.js zkey beacon <in.zkey> <out.zkey> <beaconHashHex> <numIterationsExp> [-n=name]
  */
 const fs = require('fs');
-const { groth16, exportSolidityCallData, newZKey, release } = require('./groth16');
+const { groth16, exportSolidityCallData, newZKey, beacon, release } = require('./groth16');
 
 const USAGE = 'usage: cli.js groth16 prove <circuit.zkey> <witness.wtns> <proof.json> <public.json>\n' +
               '       cli.js zkey export soliditycalldata <public.json> <proof.json>\n' +
-              '       cli.js groth16 setup|zkey new <circuit.r1cs> <pot.ptau> <circuit_0000.zkey>\n';
+              '       cli.js groth16 setup|zkey new <circuit.r1cs> <pot.ptau> <circuit_0000.zkey>\n' +
+              '       cli.js zkey beacon <in.zkey> <out.zkey> <beaconHashHex> <numIterationsExp> [-n=name]\n';
 
 async function main(argv) {
   if (argv.length === 5 && argv[0] === 'zkey' && argv[1] === 'export' && argv[2] === 'soliditycalldata') {
@@ -27,6 +30,12 @@ async function main(argv) {
   const setupArgs = argv.filter((a) => !a.startsWith('-e='));  // entropy: unused by `groth16 setup`
   if (setupArgs.length === 5 && ((argv[0] === 'zkey' && argv[1] === 'new') || (argv[0] === 'groth16' && argv[1] === 'setup'))) {
     await newZKey(setupArgs[2], setupArgs[3], setupArgs[4]);
+    return 0;
+  }
+  const named = argv.filter((a) => !/^(-n|--name)=/.test(a) && a !== '-v' && a !== '--verbose');
+  if (named.length === 6 && argv[0] === 'zkey' && argv[1] === 'beacon') {
+    const nameArg = argv.find((a) => /^(-n|--name)=/.test(a));
+    await beacon(named[2], named[3], nameArg ? nameArg.replace(/^[^=]*=/, '') : '', named[4], named[5]);
     return 0;
   }
   if (argv.length !== 6 || argv[0] !== 'groth16' || argv[1] !== 'prove') {

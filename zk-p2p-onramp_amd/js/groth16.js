@@ -149,6 +149,25 @@ async function newZKey(r1csName, ptauName, zkeyName, logger, device) {
   return out;
 }
 
+/*
+ * snarkjs' `zKey.beacon(zkeyNameOld, zkeyNameNew, name, beaconHashStr, numIterationsExp, logger)`
+ * (reference dizkus-scripts/3_gen_chunk_zkey.sh:36): delta -> k delta, L/H -> k^-1, with k
+ * derived from the beacon as snarkjs does, on the GPU.  The contribution record (section 10)
+ * is not appended: `snarkjs zkey verify` will not list this contribution.
+ */
+async function beacon(zkeyNameOld, zkeyNameNew, name, beaconHashStr, numIterationsExp, logger, device) {
+  const hex = String(beaconHashStr);
+  const bytes = /^([0-9a-fA-F]{2})+$/.test(hex) ? Buffer.from(hex, 'hex') : Buffer.alloc(0);
+  if (bytes.length === 0) throw new Error('Invalid Beacon Hash. (It must be a valid hexadecimal sequence)');
+  const e = Number(numIterationsExp);
+  if (!Number.isInteger(e) || e < 10 || e > 63) throw new Error('Invalid numIterationsExp. (Must be between 10 and 63)');
+  const out = addon.zkeyBeacon(readInput(zkeyNameOld), bytes, e, device || 0);
+  if (typeof zkeyNameNew === 'string') fs.writeFileSync(zkeyNameNew, out);
+  else if (zkeyNameNew && typeof zkeyNameNew === 'object' && zkeyNameNew.type === 'mem') zkeyNameNew.data = out;
+  if (logger && logger.info) logger.info(`zkey beacon ${name || ''}: ${out.length} bytes`);
+  return out;
+}
+
 function release() {
   for (const h of provers.values()) addon.freeProver(h);
   for (const h of memProvers.values()) addon.freeProver(h);
@@ -159,8 +178,9 @@ function release() {
 module.exports = {
   groth16: { prove, proveBatch },
   proveBatch,
-  zKey: { exportSolidityCallData, newZKey },
+  zKey: { exportSolidityCallData, newZKey, beacon },
   newZKey,
+  beacon,
   prove,
   exportSolidityCallData,
   onRampArgs,

@@ -27,6 +27,9 @@ export declare const zKey: {
   /** `snarkjs zkey new` on the GPU; writes zkeyName when given, returns the key bytes */
   newZKey(r1csName: Input, ptauName: Input, zkeyName?: string | { type: "mem"; data?: Uint8Array }, logger?: Logger,
           device?: number): Promise<Buffer>;
+  /** `snarkjs zkey beacon`'s group arithmetic on the GPU (no transcript record appended) */
+  beacon(zkeyNameOld: Input, zkeyNameNew: string | { type: "mem"; data?: Uint8Array } | undefined, name: string,
+         beaconHashStr: string, numIterationsExp: number, logger?: Logger, device?: number): Promise<Buffer>;
 };
 export declare function exportSolidityCallData(proof: Proof, publicSignals: string[]): Promise<string>;
 export declare function onRampArgs(proof: Proof, publicSignals: string[]):

@@ -10,6 +10,7 @@
  *                                                    every proof attempted, per-proof errors)
  *   freeProver(handle)
  *   zkeyNew(r1csBuffer, ptauBuffer, device?)     -> Buffer (`snarkjs zkey new`, synchronous)
+ *   zkeyBeacon(zkeyBuffer, beaconBuffer, numIterationsExp, device?) -> Buffer (`zkey beacon` math)
  *   version()
  * prove()/proveBatch() run on the libuv threadpool (napi_async_work), so the JS main
  * thread is never blocked — the same async contract as snarkjs' Promise API.
@@ -102,6 +103,45 @@ static napi_value js_zkey_new(napi_env env, napi_callback_info info) {
   uint8_t* out = NULL;
   size_t out_len = 0;
   zkp_status st = zkp_zkey_new(device, (const uint8_t*)r1cs, r1cs_len, (const uint8_t*)ptau, ptau_len, &out, &out_len);
+  if (st != ZKP_OK) return throw_status(env, st);
+  napi_value buf;
+  void* dst = NULL;
+  napi_status ns = napi_create_buffer(env, out_len, &dst, &buf);
+  if (ns == napi_ok) memcpy(dst, out, out_len);
+  zkp_buffer_free(out);
+  if (ns != napi_ok) {
+    napi_throw_error(env, NULL, "N-API call failed: napi_create_buffer");
+    return NULL;
+  }
+  return buf;
+}
+
+/* zkeyBeacon(zkeyBuffer, beaconBuffer, numIterationsExp, device?) -> Buffer: the group
+ * arithmetic of `snarkjs zkey beacon` (zkp_zkey_beacon), synchronous */
+static napi_value js_zkey_beacon(napi_env env, napi_callback_info info) {
+  size_t argc = 4;
+  napi_value argv[4];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  bool b0 = false, b1 = false;
+  uint32_t e = 0;
+  if (argc >= 3) {
+    napi_is_buffer(env, argv[0], &b0);
+    napi_is_buffer(env, argv[1], &b1);
+  }
+  if (!b0 || !b1 || napi_get_value_uint32(env, argv[2], &e) != napi_ok) {
+    napi_throw_type_error(env, NULL, "zkeyBeacon(zkeyBuffer, beaconBuffer, numIterationsExp, device?)");
+    return NULL;
+  }
+  int device = 0;
+  if (argc > 3) napi_get_value_int32(env, argv[3], &device);
+  void *zkey, *beacon;
+  size_t zkey_len, beacon_len;
+  NAPI_CALL(env, napi_get_buffer_info(env, argv[0], &zkey, &zkey_len));
+  NAPI_CALL(env, napi_get_buffer_info(env, argv[1], &beacon, &beacon_len));
+  uint8_t* out = NULL;
+  size_t out_len = 0;
+  zkp_status st = zkp_zkey_beacon(device, (const uint8_t*)zkey, zkey_len, (const uint8_t*)beacon, beacon_len, e, &out,
+                                  &out_len);
   if (st != ZKP_OK) return throw_status(env, st);
   napi_value buf;
   void* dst = NULL;
@@ -505,6 +545,7 @@ static napi_value init(napi_env env, napi_value exports) {
       {"proveBatch", NULL, js_prove_batch, NULL, NULL, NULL, napi_default, NULL},
       {"freeProver", NULL, js_free, NULL, NULL, NULL, napi_default, NULL},
       {"zkeyNew", NULL, js_zkey_new, NULL, NULL, NULL, napi_default, NULL},
+      {"zkeyBeacon", NULL, js_zkey_beacon, NULL, NULL, NULL, napi_default, NULL},
   };
   napi_define_properties(env, exports, sizeof props / sizeof props[0], props);
   return exports;

@@ -117,6 +117,9 @@ def load_library(path: str = LIB_PATH):
                                              ctypes.POINTER(sz)]
         lib.zkp_zkey_contribute.argtypes = [ctypes.c_int, u8p, sz, u8p, ctypes.POINTER(u8p), ctypes.POINTER(sz)]
         lib.zkp_zkey_new.argtypes = [ctypes.c_int, u8p, sz, u8p, sz, ctypes.POINTER(u8p), ctypes.POINTER(sz)]
+        lib.zkp_beacon_secret.argtypes = [u8p, sz, ctypes.c_uint32, u8p]
+        lib.zkp_zkey_beacon.argtypes = [ctypes.c_int, u8p, sz, u8p, sz, ctypes.c_uint32, ctypes.POINTER(u8p),
+                                        ctypes.POINTER(sz)]
         lib.zkp_buffer_free.argtypes = [u8p]
         lib.zkp_buffer_free.restype = None
         lib.zkp_prover_load_part.argtypes = [u8p, sz, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(P)]
@@ -132,7 +135,8 @@ def load_library(path: str = LIB_PATH):
                      "zkp_witness_stage", "zkp_prove_staged", "zkp_prover_instrument", "zkp_prover_kernel_stats",
                      "zkp_bench_msm", "zkp_bench_ntt", "zkp_bench_plan", "zkp_msm", "zkp_prover_msm_config",
                      "zkp_prover_load_part", "zkp_prove_partial", "zkp_proof_calldata",
-                     "zkp_prover_load_chunks", "zkp_zkey_read", "zkp_zkey_read_chunks", "zkp_zkey_contribute", "zkp_zkey_new", "zkp_prove_partial_staged", "zkp_proof_combine",
+                     "zkp_prover_load_chunks", "zkp_zkey_read", "zkp_zkey_read_chunks", "zkp_zkey_contribute", "zkp_zkey_new",
+                     "zkp_beacon_secret", "zkp_zkey_beacon", "zkp_prove_partial_staged", "zkp_proof_combine",
                      "zkp_quotient_part_staged", "zkp_prove_partial_ext_staged"):
             getattr(lib, name).restype = ctypes.c_int
         _lib = lib
@@ -489,6 +493,32 @@ def zkey_contribute(zkey: bytes, k: int, device: int = 0) -> bytes:
     out = ctypes.POINTER(ctypes.c_uint8)()
     n = ctypes.c_size_t()
     _check(lib.zkp_zkey_contribute(device, zp, zlen, kp, ctypes.byref(out), ctypes.byref(n)))
+    try:
+        return _copy_out(out, n.value)
+    finally:
+        lib.zkp_buffer_free(out)
+
+
+def beacon_secret(beacon: bytes, num_iterations_exp: int) -> int:
+    """The contribution scalar of `snarkjs zkey beacon <beacon hex> <num_iterations_exp>`
+    (host only: chained SHA-256, ChaCha20 stream, Fr.fromRng)."""
+    lib = load_library()
+    bp, bk = _buf(bytes(beacon) or b"\0")
+    k = (ctypes.c_uint8 * 32)()
+    _check(lib.zkp_beacon_secret(bp, len(beacon), num_iterations_exp, ctypes.cast(k, ctypes.POINTER(ctypes.c_uint8))))
+    return int.from_bytes(bytes(k), "little")
+
+
+def zkey_beacon(zkey: bytes, beacon: bytes, num_iterations_exp: int, device: int = 0) -> bytes:
+    """`snarkjs zkey beacon`'s group arithmetic on the GPU: delta -> k*delta with k the beacon's
+    secret (zkp_zkey_beacon; section 10 unchanged)."""
+    lib = load_library()
+    zp, zk = _buf(zkey)
+    bp, bk = _buf(bytes(beacon) or b"\0")
+    out = ctypes.POINTER(ctypes.c_uint8)()
+    n = ctypes.c_size_t()
+    _check(lib.zkp_zkey_beacon(device, zp, len(zkey), bp, len(beacon), num_iterations_exp, ctypes.byref(out),
+                               ctypes.byref(n)))
     try:
         return _copy_out(out, n.value)
     finally:
