@@ -26,6 +26,21 @@ def main(n=300):
         lines.append("mulr %s %s" % (w8(x), w8(y))); checks.append(("mulr", lambda v, x=x, y=y: v % R == x * y * inv_rp_r % R and v < 2 * R))
     # lazy subtractions feeding multiplications (field.hpp lsub / rsub), incl. extremes
     edge = [0, 1, P - 1, P, P + 1, 2 * P - 1]
+    # qreduce (add / sub / canon8 / canon4) at the extremes: a zero top limb against the largest
+    # subtrahend (the wide-borrow top limb wraps), sums at 4m - 2, values just below multiples of m
+    for a in edge + [(1 << 232) - 1, 1 << 232, 2 * P - (1 << 232)]:
+        for b in edge + [(1 << 232) - 1]:
+            lines.append("addq %s %s" % (w8(a), w8(b))); checks.append(("addq_edge", lambda v, a=a, b=b: v % P == (a + b) % P and v < 2 * P))
+            lines.append("subq %s %s" % (w8(a), w8(b))); checks.append(("subq_edge", lambda v, a=a, b=b: v % P == (a - b) % P and v < 2 * P))
+    # qreduce itself (Fr add / sub use it: FrCfg::QRED), incl. a zero top limb against the largest
+    # subtrahend (the borrow form's top limb wraps) and values just below multiples of r
+    edr = [0, 1, R - 1, R, R + 1, 2 * R - 1, (1 << 232) - 1, 1 << 232, 2 * R - (1 << 232)]
+    for a in edr + [rnd.randrange(2 * R) for _ in range(n)]:
+        for b in edr + [rnd.randrange(2 * R)]:
+            lines.append("addr %s %s" % (w8(a), w8(b))); checks.append(("addr", lambda v, a=a, b=b: v % R == (a + b) % R and v < 2 * R))
+            lines.append("subr %s %s" % (w8(a), w8(b))); checks.append(("subr", lambda v, a=a, b=b: v % R == (a - b) % R and v < 2 * R))
+    for a in [0, 1, P, 2 * P - 1, 4 * P, 5 * P - 1, (1 << 256) - 1] + [rnd.randrange(1 << 256) for _ in range(n)]:
+        lines.append("qredq %s" % w8(a)); checks.append(("qredq", lambda v, a=a: v % P == a % P and v < 6 * P // 5))
     pairs = [(rnd.randrange(2 * P), rnd.randrange(2 * P)) for _ in range(n)] + [(a, b) for a in edge for b in edge]
     for a, b in pairs:
         c = rnd.randrange(2 * P)

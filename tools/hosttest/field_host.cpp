@@ -59,6 +59,9 @@ int main() {
           y{rdf<FqCfg>(), rdf<FqCfg>()};
       Fq2 v = acc_y3(r, t, y, d); prf(v.c0); printf("\n"); prf(v.c1);
     }
+    else if (o == "addr") { Fr a = rdf<FrCfg>(), b = rdf<FrCfg>(); prf(add(a, b)); }
+    else if (o == "subr") { Fr a = rdf<FrCfg>(), b = rdf<FrCfg>(); prf(sub(a, b)); }
+    else if (o == "qredq") { Fq a = rdf<FqCfg>(); prf(qreduce(a)); }
     else if (o == "mulr") { Fr a = rdf<FrCfg>(), b = rdf<FrCfg>(); prf(mul(a, b)); }
     else if (o == "canonq") { Fq a = rdf<FqCfg>(); prf(canon(a)); }
     else if (o == "iszq") { Fq a = rdf<FqCfg>(); printf("%d", (int)is_zero(a)); }

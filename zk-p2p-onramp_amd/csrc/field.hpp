@@ -235,14 +235,49 @@ ZDEV Fe<C> cond_sub(const Fe<C>& a, const uint32_t (&M)[NL]) {
   return r;
 }
 
-// a + b, inputs < 2m -> output < 2m
+// Quotient-estimate reduction: s (limbs 0..7 in [0, 2^32 - 2^10), unnormalised; value
+// v in [0, 2^261)) -> v - q m, normalised, value < 1.2m, in ONE carry pass.  q comes from the
+// top limb alone, q = floor(s8 * floor(2^264/m) / 2^32) <= v/m (all limbs >= 0), and
+// v/m - q < 1 + 2^-3 + (low limbs) / m, so 0 <= v - q m < 1.2m.  v - q m = (v + q (2^261 - m))
+// mod 2^261: per limb one v_mad_u64_u32 (q * NM[i] + s[i] + carry < 2^39), a mask and a shift,
+// instead of a carry pass plus one or two borrow-chain conditional subtractions with selects
+// (34 vs 65-105 instructions).  A top limb that went "negative" (uint32 wrap of a wide-borrow
+// form whose true top, after the lower carries, is >= 0) has a value < 2^235 < m: q = 0.
+template <class C>
+ZDEV Fe<C> qreduce(const Fe<C>& s) {
+  const int32_t top = (int32_t)s.v[NL - 1];
+  const uint32_t q = top > 0 ? (uint32_t)(((uint64_t)(uint32_t)top * C::QK) >> 32) : 0u;
+  Fe<C> r;
+  uint32_t carry = 0;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) {
+    const uint64_t acc = (uint64_t)q * C::NM[i] + (uint64_t)(s.v[i] + carry);
+    r.v[i] = (uint32_t)acc & LMASK;
+    carry = (uint32_t)(acc >> LB);
+  }
+  return r;
+}
+
+// s (limbs < 2^31, value < 4m) -> < 2m: qreduce for Fr (C::QRED: the NTT, 3 waves/SIMD, 5 % faster
+// per transform), carry pass + one conditional subtraction for Fq, whose XYZZ kernels are
+// register-bound (qreduce's 64-bit temporaries: 124 -> 135 VGPRs in k_accumulate, 4 -> 3 waves).
+template <class C>
+ZDEV Fe<C> reduce2(Fe<C> s) {
+  if constexpr (C::QRED) {
+    return qreduce(s);
+  } else {
+    normalize(s);
+    return cond_sub(s, C::MOD2);
+  }
+}
+
+// a + b, inputs < 2m (normalised) -> output < 2m
 template <class C>
 ZDEV Fe<C> add(const Fe<C>& a, const Fe<C>& b) {
   Fe<C> s;
 #pragma unroll
   for (int i = 0; i < NL; ++i) s.v[i] = a.v[i] + b.v[i];
-  normalize(s);
-  return cond_sub(s, C::MOD2);
+  return reduce2(s);
 }
 
 // a - b, inputs < 2m -> output < 2m   (computes a + 2m - b)
@@ -251,8 +286,7 @@ ZDEV Fe<C> sub(const Fe<C>& a, const Fe<C>& b) {
   Fe<C> s;
 #pragma unroll
   for (int i = 0; i < NL; ++i) s.v[i] = a.v[i] + C::MOD2_BORROW[i] - b.v[i];
-  normalize(s);
-  return cond_sub(s, C::MOD2);
+  return reduce2(s);
 }
 
 // ---- lazy subtractions: results that only ever feed a multiplication skip the final
@@ -290,8 +324,12 @@ ZDEV Fe<C> sub_2x(const Fe<C>& a, const Fe<C>& b, const Fe<C>& c) {
   Fe<C> s;
 #pragma unroll
   for (int i = 0; i < NL; ++i) s.v[i] = a.v[i] + C::MOD6_WIDE[i] - b.v[i] - (c.v[i] << 1);
-  normalize(s);
-  return cond_sub(cond_sub(s, C::MOD4), C::MOD2);
+  if constexpr (C::QRED) {
+    return qreduce(s);
+  } else {
+    normalize(s);
+    return cond_sub(cond_sub(s, C::MOD4), C::MOD2);
+  }
 }
 
 // ---- lazily reduced accumulator x (G1 XYZZ additions): X3 = R^2 - PPP - 2Q stays in (0, 8m)
@@ -359,8 +397,12 @@ ZDEV Fe<C> add_raw_reduce(const Fe<C>& a, const Fe<C>& b) {
   Fe<C> s;
 #pragma unroll
   for (int i = 0; i < NL; ++i) s.v[i] = a.v[i] + b.v[i];
-  normalize(s);
-  return cond_sub(cond_sub(s, C::MOD4), C::MOD2);
+  if constexpr (C::QRED) {
+    return qreduce(s);
+  } else {
+    normalize(s);
+    return cond_sub(cond_sub(s, C::MOD4), C::MOD2);
+  }
 }
 
 // a - b + 6m for raw sums a, b < 4m (wide borrow form: every limb stays >= 0), normalised,
@@ -542,7 +584,9 @@ ZDEV Fq2 lsub4_lazy(const Fq2& a, const Fq2& b) { return Fq2{lsub4(a.c0, b.c0), 
 ZDEV Fq2 sqr_lazy(const Fq2& a) {
   return Fq2{mul(add_raw(a.c0, a.c1), lsub6(a.c0, a.c1)), mul(shl1_raw(a.c0), a.c1)};
 }
-// R^2 - PPP - 2Q per component (each < 2m) -> < 4m: one conditional subtraction instead of two
+// R^2 - PPP - 2Q per component (each < 2m) -> < 4m: one conditional subtraction instead of two.
+// (Not qreduce: its single 27-deep dependent chain per component measured 6 % slower in the
+// G2 accumulation, which runs at two waves per SIMD and cannot hide the latency.)
 ZDEV Fq2 sub_2x4(const Fq2& a, const Fq2& b, const Fq2& c) {
   return Fq2{cond_sub(sub_2x8(a.c0, b.c0, c.c0), FqCfg::MOD4), cond_sub(sub_2x8(a.c1, b.c1, c.c1), FqCfg::MOD4)};
 }

@@ -22,7 +22,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 PKG_ROOT = os.path.dirname(_HERE)
-LIB_PATH = os.path.join(PKG_ROOT, "lib", "libzkp_amd.so")
+LIB_PATH = os.environ.get("ZKP_LIB_PATH") or os.path.join(PKG_ROOT, "lib", "libzkp_amd.so")  # override: A/B runs
 HEADER_PATH = os.path.join(os.path.dirname(PKG_ROOT), "include", "zkp_amd.h")
 
 ZKP_OK = 0
