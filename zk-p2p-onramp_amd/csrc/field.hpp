@@ -424,6 +424,26 @@ ZDEV Fe<C> add_raw(const Fe<C>& a, const Fe<C>& b) {
   return s;
 }
 
+// DIF radix-4 unit (NTT stage pair) on normalised inputs < 2m and roots < 2m:
+//   y0 = s02 + s13, y1 = (s02 - s13) wj          (s02 = x0 + x2, s13 = x1 + x3 raw, < 4m)
+//   y2 = u wa + v wb, y3 = u wc + v wd           (u = x0 - x2, v = x1 - x3)
+// i.e. y2 = d02 + d13, y3 = (d02 - d13) wj for d02 = u wa, d13 = v wb with the combined roots
+// wc = wa wj, wd = -wb wj: each of y2, y3 is one lazily reduced sum of products (mul2), so the
+// unit takes 3 Montgomery reductions instead of 4 and no addition of products.  u = x0 - x2 + 4m
+// is raw (limbs < 2^31, < 6m) beside a normalised root, v = x1 - x3 + 2m normalised (< 4m): the
+// mul2 column sums stay < 9*2^60 + 18*2^58 < 2^64, u wa + v wb < 20 m^2 (output < 2m).
+template <class C>
+ZDEV void r4_dif(const Fe<C>& x0, const Fe<C>& x1, const Fe<C>& x2, const Fe<C>& x3, const Fe<C>& wa,
+                 const Fe<C>& wb, const Fe<C>& wc, const Fe<C>& wd, const Fe<C>& wj, Fe<C>& y0, Fe<C>& y1,
+                 Fe<C>& y2, Fe<C>& y3) {
+  const Fe<C> s02 = add_raw(x0, x2), s13 = add_raw(x1, x3);
+  const Fe<C> u = rsub(x0, x2), v = lsub(x1, x3);
+  y0 = add_raw_reduce(s02, s13);
+  y1 = mul(sub_raw6(s02, s13), wj);
+  y2 = mul2(u, wa, v, wb);
+  y3 = mul2(u, wc, v, wd);
+}
+
 template <class C>
 ZDEV Fe<C> dbl(const Fe<C>& a) { return add(a, a); }
 

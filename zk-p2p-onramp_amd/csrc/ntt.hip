@@ -15,7 +15,21 @@ constexpr int TPB = 256;
 constexpr int LOG_TILE = 10;  // elements per workgroup tile (1024, 36 KiB of LDS)
 constexpr int LOC_LOG = 10;   // local-root table: w_1024^e, e < 512
 constexpr int MAX_PASS_BITS = 8;
-constexpr int MAX_TW = 1 << (MAX_PASS_BITS - 1);  // stage roots of a 2^b-point DFT, b <= 8
+// Radix-4 unit variant (A/B build knobs): ZKP_NTT_MUL2 = 1 computes y2, y3 as lazily reduced sums of
+// products with combined roots (field.hpp r4_dif, full-circle root table), 0 the four-multiply unit
+// (half-circle table); ZKP_NTT_PACKED = 1 keeps the LDS roots as 8 packed words (unpacked per use);
+// ZKP_NTT_WPE bounds the waves per SIMD the register allocation targets (0 = compiler's choice).
+#ifndef ZKP_NTT_MUL2
+#define ZKP_NTT_MUL2 0
+#endif
+#ifndef ZKP_NTT_PACKED
+#define ZKP_NTT_PACKED 0
+#endif
+#ifndef ZKP_NTT_WPE
+#define ZKP_NTT_WPE 0
+#endif
+constexpr int MAX_TW = ZKP_NTT_MUL2 ? (1 << MAX_PASS_BITS) : (1 << (MAX_PASS_BITS - 1));  // stage roots, b <= 8
+constexpr int RW = ZKP_NTT_PACKED ? 8 : NL;  // LDS words per root
 
 __device__ __forceinline__ uint32_t brev(uint32_t x, int b) { return __builtin_bitreverse32(x) >> (32 - b); }
 
@@ -34,14 +48,38 @@ struct Tile {
   int lm, b, lc, lbt;
 };
 
-// the per-stage roots w_(2^b)^j, j < 2^(b-1), staged in LDS (9-limb SoA)
+// the stage roots w_(2^b)^j staged in LDS (SoA): j < 2^(b-1), and with ZKP_NTT_MUL2 the full
+// circle j < 2^b (w^(j + 2^(b-1)) = -w^j: the combined roots of r4_dif reach every exponent)
+__device__ __forceinline__ void put_root(uint32_t* __restrict__ ltw, int j, const Fr& x) {
+#if ZKP_NTT_PACKED
+  uint32_t w[8];
+  pack(x, w);
+#pragma unroll
+  for (int l = 0; l < 8; ++l) ltw[l * MAX_TW + j] = w[l];
+#else
+#pragma unroll
+  for (int l = 0; l < NL; ++l) ltw[l * MAX_TW + j] = x.v[l];
+#endif
+}
 __device__ __forceinline__ void stage_roots(uint32_t* __restrict__ ltw, const uint32_t* __restrict__ loc, int b) {
   const int TW = 1 << (b - 1);
   for (int j = threadIdx.x; j < TW; j += TPB) {
     const Fr x = load_fe<FrCfg>(loc + (size_t)(j << (LOC_LOG - b)) * 8);
-#pragma unroll
-    for (int l = 0; l < NL; ++l) ltw[l * MAX_TW + j] = x.v[l];
+    put_root(ltw, j, x);
+    if (ZKP_NTT_MUL2) put_root(ltw, j + TW, neg(x));
   }
+}
+
+// LDS data-tile swizzle: element e lives at word e ^ S(e), S(e) = (h ^ 2h ^ 8h) mod 32, h = e >> 5
+// (an XOR of bits 5.. into the bank bits 0..4).  ds_read_b32 / ds_write_b32 banks are word mod 32 per
+// 32-lane half; unswizzled, the later radix-4 rounds hit 2- and 4-way conflicts and the digit-reversed
+// reads of the store phase 8-way ones.  This S makes every access phase of every tile geometry the
+// NTT uses (b, lc, lbt for 2^12..2^23) conflict-free (searched by simulating the bank mapping of all
+// the phases).  S is linear over GF(2) in the bits of e, so for x whose bits are disjoint from e0's,
+// swz(e0 | x) = swz(e0) ^ swz(x): a radix-4 unit swizzles e0 once and XORs wave-uniform row offsets.
+__device__ __forceinline__ int swz(int e) {
+  const int h = e >> 5;
+  return e ^ ((h ^ (h << 1) ^ (h << 3)) & 31);
 }
 
 __device__ __forceinline__ Fr lds_get(const uint32_t* __restrict__ lds, int E, int e) {
@@ -55,16 +93,22 @@ __device__ __forceinline__ void lds_put(uint32_t* __restrict__ lds, int E, int e
   for (int l = 0; l < NL; ++l) lds[l * E + e] = x.v[l];
 }
 __device__ __forceinline__ Fr root(const uint32_t* __restrict__ ltw, uint32_t j) {
+#if ZKP_NTT_PACKED
+  uint32_t w[8];
+#pragma unroll
+  for (int l = 0; l < 8; ++l) w[l] = ltw[l * MAX_TW + j];
+  return unpack<FrCfg>(w);
+#else
   Fr w;
 #pragma unroll
   for (int l = 0; l < NL; ++l) w.v[l] = ltw[l * MAX_TW + j];
   return w;
+#endif
 }
 // DIF butterfly output d = (x - y) w_j, with w_0 = 1 (x - y only feeds the multiply: raw)
 __device__ __forceinline__ Fr bfly_d(const Fr& x, const Fr& y, const uint32_t* __restrict__ ltw, uint32_t j) {
   return j ? mul(rsub(x, y), root(ltw, j)) : sub(x, y);
 }
-
 // b radix-2 DIF stages on the LDS tile (rows natural in, bit-reversed out), done two at a
 // time as radix-4 groups in registers (half the LDS traffic and barriers of radix-2):
 // rows r0 + {0, H/2, H, 3H/2} of stage t (span H) and t+1 (span H/2), r0 = grp 2H + i.
@@ -81,25 +125,51 @@ __device__ __forceinline__ void dft_stages(uint32_t* __restrict__ lds, const uin
       const uint32_t i = bq & (Hh - 1), grp = bq >> (lhalf - 1);
       const uint32_t r0 = (grp << (lhalf + 1)) | i;
       const int base = (int)(bl << (b + lc)) + (int)col;
-      const int e0 = base + (int)(r0 << lc), st = (int)(Hh << lc);
-      const Fr x0 = lds_get(lds, E, e0), x1 = lds_get(lds, E, e0 + st), x2 = lds_get(lds, E, e0 + 2 * st),
-               x3 = lds_get(lds, E, e0 + 3 * st);
-      // stage t: (x0, x2) with w_(2H)^i, (x1, x3) with w_(2H)^(i + H/2)
+      const int st = (int)(Hh << lc);
+      // swizzled rows e0 + k st = e0 | k st (disjoint bits): p0 ^ swz(k st)
+      const int p0 = swz(base + (int)(r0 << lc)), p1 = p0 ^ swz(st), p2 = p0 ^ swz(2 * st), p3 = p0 ^ swz(3 * st);
+      const Fr x0 = lds_get(lds, E, p0), x1 = lds_get(lds, E, p1), x2 = lds_get(lds, E, p2), x3 = lds_get(lds, E, p3);
+      // stage t: (x0, x2) with w_(2H)^i, (x1, x3) with w_(2H)^(i + H/2); stage t+1: (s02, s13)
+      // and (d02, d13), both with w_H^i.  Roots as exponents of w_(2^b) (stage t: i << t).
+#if ZKP_NTT_MUL2
+      if (Hh > 1) {
+        // y0 = s02 + s13 and y1 = (s02 - s13) w_H^i with the sums raw (< 4m, one reduction);
+        // y2 = d02 + d13 and y3 = (d02 - d13) w_H^i as lazily reduced sums of products over
+        // u = x0 - x2 and v = x1 - x3 with combined roots (r4_dif): 3 reductions per unit, not 4
+        const uint32_t ia = i << t, ib = (i + Hh) << t, ic = (3 * i) << t;
+        const uint32_t id = ((3 * i + 3 * Hh) << t) & ((1u << b) - 1);  // -w^(3i + H/2) = w^(3i + 3H/2)
+        Fr y0, y1, y2, y3;
+        r4_dif(x0, x1, x2, x3, root(ltw, ia), root(ltw, ib), root(ltw, ic), root(ltw, id), root(ltw, i << (t + 1)),
+               y0, y1, y2, y3);
+        lds_put(lds, E, p0, y0);
+        lds_put(lds, E, p1, y1);
+        lds_put(lds, E, p2, y2);
+        lds_put(lds, E, p3, y3);
+      } else {  // last pair (span 1, i = 0): roots 1 except w_(2H)^(H/2) for (x1, x3)
+        const Fr d02 = sub(x0, x2);
+        const Fr d13 = mul(rsub(x1, x3), root(ltw, Hh << t));
+        const Fr s02 = add(x0, x2), s13 = add(x1, x3);
+        lds_put(lds, E, p0, add(s02, s13));
+        lds_put(lds, E, p1, sub(s02, s13));
+        lds_put(lds, E, p2, add(d02, d13));
+        lds_put(lds, E, p3, sub(d02, d13));
+      }
+#else
       const Fr d02 = bfly_d(x0, x2, ltw, i << t);
       const Fr d13 = bfly_d(x1, x3, ltw, (i + Hh) << t);
-      // stage t+1: (s02, s13) and (d02, d13), both with w_H^i
       const uint32_t j = i << (t + 1);
       if (Hh > 1) {  // the sums stay raw (< 4m) and meet one reduction; w_H^0 = 1 (Montgomery) for i = 0
         const Fr s02 = add_raw(x0, x2), s13 = add_raw(x1, x3);
-        lds_put(lds, E, e0, add_raw_reduce(s02, s13));
-        lds_put(lds, E, e0 + st, mul(sub_raw6(s02, s13), root(ltw, j)));
+        lds_put(lds, E, p0, add_raw_reduce(s02, s13));
+        lds_put(lds, E, p1, mul(sub_raw6(s02, s13), root(ltw, j)));
       } else {  // last pair (span 1): no multiply in stage t+1
         const Fr s02 = add(x0, x2), s13 = add(x1, x3);
-        lds_put(lds, E, e0, add(s02, s13));
-        lds_put(lds, E, e0 + st, sub(s02, s13));
+        lds_put(lds, E, p0, add(s02, s13));
+        lds_put(lds, E, p1, sub(s02, s13));
       }
-      lds_put(lds, E, e0 + 2 * st, add(d02, d13));
-      lds_put(lds, E, e0 + 3 * st, bfly_d(d02, d13, ltw, j));
+      lds_put(lds, E, p2, add(d02, d13));
+      lds_put(lds, E, p3, bfly_d(d02, d13, ltw, j));
+#endif
     }
     __syncthreads();
   }
@@ -107,10 +177,10 @@ __device__ __forceinline__ void dft_stages(uint32_t* __restrict__ lds, const uin
     for (int q = threadIdx.x; q < (E >> 1); q += TPB) {
       const uint32_t col = (uint32_t)q & (C - 1), bq = ((uint32_t)q >> lc) & ((1u << (b - 1)) - 1);
       const uint32_t bl = (uint32_t)q >> (lc + b - 1);
-      const int e0 = (int)(bl << (b + lc)) + (int)((bq << 1) << lc) + (int)col, e1 = e0 + (int)C;
-      const Fr x = lds_get(lds, E, e0), y = lds_get(lds, E, e1);
-      lds_put(lds, E, e0, add(x, y));
-      lds_put(lds, E, e1, sub(x, y));  // span 1: the root is w_2^0 = 1
+      const int p0 = swz((int)(bl << (b + lc)) + (int)((bq << 1) << lc) + (int)col), p1 = p0 ^ swz((int)C);
+      const Fr x = lds_get(lds, E, p0), y = lds_get(lds, E, p1);
+      lds_put(lds, E, p0, add(x, y));
+      lds_put(lds, E, p1, sub(x, y));  // span 1: the root is w_2^0 = 1
     }
     __syncthreads();
   }
@@ -147,16 +217,20 @@ __device__ __forceinline__ int brev_src(const Tile& T, int e) {
 // 2: the fused innermost pair of coset_extend (lm == b): inverse-root DFT, coset key
 //    (table by digit-reversed position), forward-root DFT on one LDS-resident tile.
 // tw: w_(2^lm)^(col*row) by position in block (null when n2 == 1).
+#if ZKP_NTT_WPE
+#define NTT_WPE_ATTR __attribute__((amdgpu_waves_per_eu(ZKP_NTT_WPE)))
+#else
+#define NTT_WPE_ATTR
+#endif
 template <int MODE>
-__global__ __launch_bounds__(TPB) void k_ntt(uint32_t* __restrict__ data, Tile T, const uint32_t* __restrict__ tw,
+__global__ __launch_bounds__(TPB) NTT_WPE_ATTR void k_ntt(uint32_t* __restrict__ data, Tile T, const uint32_t* __restrict__ tw,
                                              const uint32_t* __restrict__ locA, const uint32_t* __restrict__ locB,
                                              const uint32_t* __restrict__ coset) {
   __shared__ uint32_t lds[NL << LOG_TILE];  // SoA: lds[limb * E + element]
-  __shared__ uint32_t ltw[(MODE == 2 ? 2 : 1) * NL * MAX_TW];
+  __shared__ uint32_t ltw[RW * MAX_TW];
   const int E = 1 << (T.b + T.lc + T.lbt);
   const uint32_t tile = blockIdx.x;
   stage_roots(ltw, locA, T.b);
-  if (MODE == 2) stage_roots(ltw + NL * MAX_TW, locB, T.b);
   for (int e = threadIdx.x; e < E; e += TPB) {
     size_t g;
     uint32_t pos;
@@ -164,7 +238,7 @@ __global__ __launch_bounds__(TPB) void k_ntt(uint32_t* __restrict__ data, Tile T
     Fr x = load_fe<FrCfg>(data + g * 8);
     if (MODE == 1 && tw) x = mul(x, load_fe<FrCfg>(tw + (size_t)pos * 8));
 #pragma unroll
-    for (int l = 0; l < NL; ++l) lds[l * E + e] = x.v[l];
+    for (int l = 0; l < NL; ++l) lds[l * E + swz(e)] = x.v[l];
   }
   __syncthreads();
   dft_stages(lds, ltw, E, T.b, T.lc);
@@ -174,7 +248,7 @@ __global__ __launch_bounds__(TPB) void k_ntt(uint32_t* __restrict__ data, Tile T
     Fr v[(1 << LOG_TILE) / TPB];
     int idx = 0;
     for (int e = threadIdx.x; e < E; e += TPB, ++idx) {
-      const int src = brev_src(T, e);
+      const int src = swz(brev_src(T, e));
       Fr x;
 #pragma unroll
       for (int l = 0; l < NL; ++l) x.v[l] = lds[l * E + src];
@@ -184,16 +258,17 @@ __global__ __launch_bounds__(TPB) void k_ntt(uint32_t* __restrict__ data, Tile T
       v[idx] = mul(x, load_fe<FrCfg>(coset + g * 8));
     }
     __syncthreads();
+    stage_roots(ltw, locB, T.b);  // the forward roots replace the inverse ones (no reader until the next barrier)
     idx = 0;
     for (int e = threadIdx.x; e < E; e += TPB, ++idx) {
 #pragma unroll
-      for (int l = 0; l < NL; ++l) lds[l * E + e] = v[idx].v[l];
+      for (int l = 0; l < NL; ++l) lds[l * E + swz(e)] = v[idx].v[l];
     }
     __syncthreads();
-    dft_stages(lds, ltw + NL * MAX_TW, E, T.b, T.lc);
+    dft_stages(lds, ltw, E, T.b, T.lc);
   }
   for (int e = threadIdx.x; e < E; e += TPB) {
-    const int src = brev_src(T, e);
+    const int src = swz(brev_src(T, e));
     Fr x;
 #pragma unroll
     for (int l = 0; l < NL; ++l) x.v[l] = lds[l * E + src];
