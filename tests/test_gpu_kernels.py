@@ -48,7 +48,9 @@ def _blob(pts, scal):
     return b"".join(bn254.g1_to_lem(p) for p in pts), b"".join(bn254.int_to_le(x) for x in scal)
 
 
-def test_msm_g1_edge_distributions():
+@pytest.mark.parametrize("dense", ["1", "0"])  # kernel-level default (dense, hand-written sort) and compacted
+def test_msm_g1_edge_distributions(monkeypatch, dense):
+    monkeypatch.setenv("ZKP_MSM_DENSE", dense)
     pts = _pts(300, 99)
     cases = {
         "empty": ([], []),
@@ -124,6 +126,7 @@ def test_msm_dense_counting_sort_large(monkeypatch):
     pts = [base[i % 64] for i in range(n)]
     sc = [rng.fr() for _ in range(n)]
     pb, sb = _blob(pts, sc)
+    monkeypatch.setenv("ZKP_MSM_DENSE", "0")
     want = zkp_amd.msm_g1(pb, sb, window_bits=20)
     monkeypatch.setenv("ZKP_MSM_DENSE", "1")
     assert zkp_amd.msm_g1(pb, sb, window_bits=20) == want
@@ -173,8 +176,10 @@ def test_quotient_golden(golden_dir, name):
 # Pippenger parameter variants: window bits c and base-table depth T (T = W: one shared
 # bucket set over precomputed 2^(c t) P rows; T = 1: one bucket group per window;
 # 1 < T < W: several groups folded by Horner with shift c*T).  Bit-exact vs the oracle.
+@pytest.mark.parametrize("dense", ["1", "0"])
 @pytest.mark.parametrize("c,depth", [(0, 1), (5, 0), (5, 3), (8, 7), (13, 0), (2, 0), (20, 0)])
-def test_msm_g1_params(c, depth):
+def test_msm_g1_params(monkeypatch, c, depth, dense):
+    monkeypatch.setenv("ZKP_MSM_DENSE", dense)
     pts = _pts(200, 5)
     rng = circuit.SplitMix64(6, 1)
     sc = [rng.fr() for _ in range(200)]

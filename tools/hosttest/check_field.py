@@ -93,6 +93,26 @@ def main(n=300):
         s02, s13 = x0 + x2, x1 + x3
         checks.append(("r4r_sum", lambda v, t=s02 + s13: v % R == t % R and v < 2 * R))
         checks.append(("r4r_dif", lambda v, t=(s02 - s13) * wv: v % R == t * inv_rp_r % R and v < 2 * R))
+    # Shoup product by a constant (field.hpp mul_shoup): a up to 2^261 with raw limbs < 2^31 (a borrow-
+    # form difference), w < r plain, wq = floor(w 2^261 / r); result congruent and < 3r
+    def l9(x, raw=False):
+        if raw:  # limbs just below 2^31 where possible, same value: borrow 2^29 from each next limb
+            limbs = [(x >> (29 * i)) & ((1 << 29) - 1) for i in range(9)]
+            limbs[8] = x >> 232
+            for i in range(8):
+                if limbs[i + 1] >= 3:
+                    limbs[i] += 3 << 29
+                    limbs[i + 1] -= 3
+            assert sum(v << (29 * i) for i, v in enumerate(limbs)) == x and max(limbs) < 1 << 31
+        else:
+            limbs = [(x >> (29 * i)) & ((1 << 29) - 1) for i in range(8)] + [x >> 232]
+        return " ".join("%x" % v for v in limbs)
+    sh = [(rnd.randrange(1 << 261), rnd.randrange(R)) for _ in range(n)]
+    sh += [((1 << 261) - 1, R - 1), (0, R - 1), ((1 << 261) - 1, 1), (3 * R - 1, R - 1), (7 * R, R - 2), (1, 0)]
+    for k, (a, wv) in enumerate(sh):
+        wq = (wv << 261) // R
+        lines.append("shoupr %s %s %s" % (l9(a, raw=k % 2 == 1), w8(wv), l9(wq)))
+        checks.append(("shoupr", lambda z, a=a, wv=wv: z % R == a * wv % R and z < 3 * R))
     # NTT radix-4 unit (field.hpp r4_dif): inputs and roots < 2m, incl. all-extreme operands
     r4 = [[rnd.randrange(2 * R) for _ in range(9)] for _ in range(n)]
     r4 += [[2 * R - 1] * 9, [0] * 9, [2 * R - 1, 0, 0, 2 * R - 1] + [2 * R - 1] * 5,

@@ -11,6 +11,8 @@ static void rd(uint32_t w[8]) { for (int i = 0; i < 8; ++i) if (scanf("%x", &w[i
 static void pr(const uint32_t w[8]) { for (int i = 0; i < 8; ++i) printf("%08x ", w[i]); }
 template <class C> static Fe<C> rdf() { uint32_t w[8]; rd(w); return unpack<C>(w); }
 template <class C> static void prf(const Fe<C>& x) { uint32_t w[8]; pack(x, w); pr(w); }
+// 9 hex 29-bit limbs (values up to 2^261, e.g. a Shoup quotient)
+template <class C> static Fe<C> rdl() { Fe<C> x; for (int i = 0; i < NL; ++i) if (scanf("%x", &x.v[i]) != 1) exit(1); return x; }
 
 int main() {
   char op[32];
@@ -39,6 +41,10 @@ int main() {
       Fr x0 = rdf<FrCfg>(), x1 = rdf<FrCfg>(), x2 = rdf<FrCfg>(), x3 = rdf<FrCfg>(), w = rdf<FrCfg>();
       const Fr s02 = add_raw(x0, x2), s13 = add_raw(x1, x3);
       prf(add_raw_reduce(s02, s13)); printf("\n"); prf(mul(sub_raw6(s02, s13), w));
+    }
+    else if (o == "shoupr") {  // a (limbs), w (words, plain), wq (limbs): a w mod r in [0, 3r)
+      Fr a = rdl<FrCfg>(), w = rdf<FrCfg>(), wq = rdl<FrCfg>();
+      prf(mul_shoup(a, w, wq));
     }
     else if (o == "r4d") {  // NTT radix-4 unit r4_dif: prints y0, y1, y2, y3
       Fr x0 = rdf<FrCfg>(), x1 = rdf<FrCfg>(), x2 = rdf<FrCfg>(), x3 = rdf<FrCfg>();

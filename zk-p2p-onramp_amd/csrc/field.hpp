@@ -89,6 +89,42 @@ ZDEV Fe<C> mul(const Fe<C>& a, const Fe<C>& b) {
   return r;
 }
 
+// Product by a CONSTANT with a precomputed quotient (Shoup): a w mod m for w < m given as plain
+// limbs and wq = floor(w 2^261 / m) (both normalised, 9 limbs).  q = floor(a wq / 2^261) from the
+// product columns 7..17 only (the dropped columns 0..6 sum to < 2^237, so q is the exact floor or
+// one less), then a w - q m = (a w + q (2^261 - m)) mod 2^261 from the low columns 0..8.  Since
+// a w / m - a wq / 2^261 < a / 2^261 <= 1, the result is in [0, 3m).  a: limbs < 2^31 (a raw sum
+// or borrow-form difference is fine), value < 2^261.  A Montgomery-form a stays in Montgomery
+// form (w is plain).  143 v_mad_u64_u32 and no per-column quotient digits, against 162 mads plus
+// 9 v_mul_lo_u32 for mul(); NTT roots, twiddles and the coset key are all constants.
+template <class C>
+ZDEV Fe<C> mul_shoup(const Fe<C>& a, const Fe<C>& w, const Fe<C>& wq) {
+  uint32_t q[NL];
+  uint64_t acc = 0;
+#pragma unroll
+  for (int c = 7; c < 2 * NL - 1; ++c) {
+#pragma unroll
+    for (int i = (c - NL + 1 > 0 ? c - NL + 1 : 0); i <= (c < NL - 1 ? c : NL - 1); ++i)
+      acc += (uint64_t)a.v[i] * wq.v[c - i];
+    if (c >= NL) q[c - NL] = (uint32_t)acc & LMASK;
+    acc >>= LB;
+  }
+  q[NL - 1] = (uint32_t)acc;  // columns 9..16 give q's limbs 0..7, the carry out its top limb (q < 2^261)
+  Fe<C> r;
+  acc = 0;
+#pragma unroll
+  for (int c = 0; c < NL; ++c) {
+#pragma unroll
+    for (int i = 0; i <= c; ++i) {
+      acc += (uint64_t)a.v[i] * w.v[c - i];
+      acc += (uint64_t)q[i] * C::NM[c - i];
+    }
+    r.v[c] = (uint32_t)acc & LMASK;
+    acc >>= LB;
+  }
+  return r;
+}
+
 // Montgomery product of a SUM of two products, (a*b + c*d)/2^261 mod m, with ONE
 // reduction ("lazy reduction"): the a*b, c*d and m*MOD partial products of a column
 // accumulate together.  All four operands normalised (limbs < 2^29; column sums

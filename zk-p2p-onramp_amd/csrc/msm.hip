@@ -199,6 +199,38 @@ __global__ __launch_bounds__(TPB) void k_subset_level(const uint32_t* __restrict
   msmk::subset_level<F>(blockIdx.x * TPB + threadIdx.x, in, nseg, n_in, fan, out);
 }
 
+// (no waves-per-SIMD bound: a latency-bound tree, one wave per SIMD suffices; bounding the G2 variant
+// to two waves spills ~290 dwords)
+template <class F>
+__global__ __launch_bounds__(msmk::TREE_TPB) void k_subset_tree_first(
+    const uint32_t* __restrict__ s_in, const uint32_t* __restrict__ t_in, uint32_t lgP, uint32_t nch,
+    uint32_t* __restrict__ out) {
+  __shared__ uint32_t lds[msmk::XyzzLimbs<F>::N * (msmk::TREE_TPB / 2)];
+  msmk::subset_tree_first<F>(s_in, t_in, lgP, nch, blockIdx.y, blockIdx.x, lds, out);
+}
+template <class F>
+__global__ __launch_bounds__(msmk::TREE_TPB) void k_subset_tree_next(
+    const uint32_t* __restrict__ in, uint32_t n_in, uint32_t n_out, uint32_t* __restrict__ out) {
+  __shared__ uint32_t lds[msmk::XyzzLimbs<F>::N * (msmk::TREE_TPB / 2)];
+  msmk::subset_tree_next<F>(in, n_in, n_out, blockIdx.y, blockIdx.x, lds, out);
+}
+// largest first-level tree grid (workgroups); larger subset sums (the proof's MSMs) start with
+// full-lane fan-in chains (ZKP_TREE_FIRST_MAX overrides)
+static size_t tree_first_max() {
+  static const size_t v = [] {
+    const char* e = std::getenv("ZKP_TREE_FIRST_MAX");
+    return e ? (size_t)std::atol(e) : (size_t)512;
+  }();
+  return v;
+}
+static bool subset_tree() {
+  static const bool on = [] {
+    const char* e = std::getenv("ZKP_SUBSET_TREE");
+    return !(e && std::atoi(e) == 0);
+  }();
+  return on;
+}
+
 // Bucket-key sort: rocprim onesweep with 9-bit digits (512-way, 2 passes for the 17/18-bit keys
 // of c = 18/19) instead of the default 8-bit (3 passes): measured 35.7 vs 36.1 ms per proof;
 // other key widths keep the default (e.g. 15 bits: 2 passes either way, default faster).
@@ -423,10 +455,32 @@ void run_finish(const MsmPlan& plan, uint32_t* part_a, uint32_t* part_b, uint32_
   const uint32_t M = (uint32_t)prm.M, lgP = (uint32_t)prm.lgP(), K = (uint32_t)prm.K(), fan = (uint32_t)prm.L;
   hipLaunchKernelGGL(k_reduce_segments<F>, dim3(grid_for((size_t)G * (half / M))), dim3(TPB), 0, st, buckets, G, half,
                      M, seg_s, seg_t);
+  int cur = 0;
+  if (subset_tree()) {  // workgroup LDS trees: 2 * TREE_TPB values per workgroup and launch level
+    constexpr uint32_t CH = 2 * msmk::TREE_TPB;
+    uint32_t n = ((1u << lgP) + CH - 1) / CH;
+    if ((size_t)G * K * n <= tree_first_max()) {  // about one round of workgroups: the tree from the inputs
+      hipLaunchKernelGGL(k_subset_tree_first<F>, dim3(n, G * K), dim3(msmk::TREE_TPB), 0, st, seg_s, seg_t, lgP, n,
+                         sub[0]);
+    } else {  // many inputs (the H MSM: K x 2^16): full-lane fan-in chains first, trees above them
+      n = (((1u << lgP) + 2 * fan - 1) / (2 * fan));
+      hipLaunchKernelGGL(k_subset_first<F>, dim3(grid_for((size_t)G * K * n)), dim3(TPB), 0, st, seg_s, seg_t, G,
+                         lgP, fan, sub[0]);
+    }
+    while (n > 1) {
+      const uint32_t next = (n + CH - 1) / CH;
+      hipLaunchKernelGGL(k_subset_tree_next<F>, dim3(next, G * K), dim3(msmk::TREE_TPB), 0, st, sub[cur], n, next,
+                         sub[cur ^ 1]);
+      cur ^= 1;
+      n = next;
+    }
+    HIPX(hipGetLastError());
+    HIPX(hipMemcpyAsync(d_out, sub[cur], (size_t)G * K * xyzz_bytes, hipMemcpyDeviceToDevice, st));
+    return;
+  }
   uint32_t n = (((1u << lgP) + 2 * fan - 1) / (2 * fan));
   hipLaunchKernelGGL(k_subset_first<F>, dim3(grid_for((size_t)G * K * n)), dim3(TPB), 0, st, seg_s, seg_t, G, lgP,
                      fan, sub[0]);
-  int cur = 0;
   while (n > 1) {
     const uint32_t next = (n + fan - 1) / fan;
     hipLaunchKernelGGL(k_subset_level<F>, dim3(grid_for((size_t)G * K * next)), dim3(TPB), 0, st, sub[cur], G * K,
@@ -751,7 +805,9 @@ MsmEngine::MsmEngine(Curve curve, const MsmParams& prm, size_t max_n, hipStream_
   const size_t nseg = (size_t)prm_.groups * (half / prm_.M);
   HIPX(hipMalloc(&seg_s_, nseg * xyzz_words * 4));
   HIPX(hipMalloc(&seg_t_, nseg * xyzz_words * 4));
-  const size_t n1 = (size_t)prm_.groups * prm_.K() * (((half / prm_.M) + 2 * prm_.L - 1) / (2 * prm_.L));
+  const size_t n1 = (size_t)prm_.groups * prm_.K() *
+                    std::max(((half / prm_.M) + 2 * prm_.L - 1) / (2 * prm_.L),
+                             ((half / prm_.M) + 2 * msmk::TREE_TPB - 1) / (2 * msmk::TREE_TPB));
   for (int i = 0; i < 2; ++i) HIPX(hipMalloc(&sub_[i], n1 * xyzz_words * 4));
   for (auto& e : ev_) {
     HIPX(hipEventCreate(&e[0]));

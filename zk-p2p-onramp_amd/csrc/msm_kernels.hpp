@@ -135,7 +135,11 @@ ZDEV void accumulate(uint32_t i, const uint32_t* __restrict__ points, const uint
   }
   for (; j < s1; ++j) {
     const uint32_t v = vals[j];
+#ifdef ZKP_ACC_GATHER_MASK  // latency probe only (wrong results): gathers confined to a cache-resident slice
+    xyzz_add_aff(acc, load_aff<F>(points, v & ZKP_ACC_GATHER_MASK), (v >> 31) != 0);
+#else
     xyzz_add_aff(acc, load_aff<F>(points, v & 0x7fffffffu), (v >> 31) != 0);
+#endif
   }
   store_xyzz(out, t, acc);
 }
@@ -263,6 +267,111 @@ ZDEV void subset_level(uint32_t id, const uint32_t* __restrict__ in, uint32_t ns
   Xyzz<F> acc = xyzz_inf<F>();
   for (uint32_t i = j * fan; i < umin((j + 1) * fan, n_in); ++i) xyzz_add(acc, load_xyzz<F>(in, (size_t)seg * n_in + i));
   store_xyzz(out, id, acc);
+}
+
+// ---- subset sums by workgroup LDS trees (ZKP_SUBSET_TREE, default): a workgroup of TREE_TPB
+// threads sums 2 * TREE_TPB consecutive values of one sum -- two loads and one addition per
+// thread, then log2(TREE_TPB) halving levels through LDS -- so the sequential chain of a sum
+// over P/2 values is ~1 + 8 additions per launch and ceil(log_512(P/2)) launches, instead of
+// fan-in-L chains over ceil(log_L(P/2)) dependent launches (the finish is latency-bound: every
+// sequential full addition costs ~5 us on a lightly loaded SIMD).
+constexpr int TREE_TPB = 256;
+template <class F>
+struct XyzzLimbs;  // 32-bit words of one XYZZ point in the 9-limb compute form
+template <>
+struct XyzzLimbs<Fq> {
+  static constexpr int N = 4 * NL;
+};
+template <>
+struct XyzzLimbs<Fq2> {
+  static constexpr int N = 8 * NL;
+};
+// LDS slot layout: word k of slot s at lds[k * (TREE_TPB / 2) + s] (consecutive slots in
+// consecutive banks)
+ZDEV void tree_put(uint32_t* lds, int& k, int slot, const Fq& x) {
+#pragma unroll
+  for (int l = 0; l < NL; ++l) lds[(k + l) * (TREE_TPB / 2) + slot] = x.v[l];
+  k += NL;
+}
+ZDEV void tree_put(uint32_t* lds, int& k, int slot, const Fq2& x) {
+  tree_put(lds, k, slot, x.c0);
+  tree_put(lds, k, slot, x.c1);
+}
+ZDEV void tree_get(const uint32_t* lds, int& k, int slot, Fq& x) {
+#pragma unroll
+  for (int l = 0; l < NL; ++l) x.v[l] = lds[(k + l) * (TREE_TPB / 2) + slot];
+  k += NL;
+}
+ZDEV void tree_get(const uint32_t* lds, int& k, int slot, Fq2& x) {
+  tree_get(lds, k, slot, x.c0);
+  tree_get(lds, k, slot, x.c1);
+}
+// the workgroup's sum of every thread's v (valid in thread 0); lds: XyzzLimbs<F>::N * TREE_TPB / 2
+// words.  The lazily reduced accumulator x is a valid addition operand as it is (mul operand).
+template <class F>
+__device__ __forceinline__ Xyzz<F> wg_tree_sum(Xyzz<F> v, uint32_t* lds) {
+  const int t = (int)threadIdx.x;
+  for (int sh = TREE_TPB / 2; sh >= 1; sh >>= 1) {
+    if (t >= sh && t < 2 * sh) {
+      int k = 0;
+      tree_put(lds, k, t - sh, v.x);
+      tree_put(lds, k, t - sh, v.y);
+      tree_put(lds, k, t - sh, v.zz);
+      tree_put(lds, k, t - sh, v.zzz);
+    }
+    __syncthreads();
+    if (t < sh) {
+      Xyzz<F> q;
+      int k = 0;
+      tree_get(lds, k, t, q.x);
+      tree_get(lds, k, t, q.y);
+      tree_get(lds, k, t, q.zz);
+      tree_get(lds, k, t, q.zzz);
+      xyzz_add(v, q);
+    }
+    __syncthreads();
+  }
+  return v;
+}
+
+// first tree level of the K = lgP + 1 subset sums of group g (seg = g * K + b): chunk `chunk`
+// (2 * TREE_TPB values) of sum b -> out[seg * nch + chunk]
+template <class F>
+__device__ __forceinline__ void subset_tree_first(const uint32_t* __restrict__ s_in, const uint32_t* __restrict__ t_in,
+                                                  uint32_t lgP, uint32_t nch, uint32_t seg, uint32_t chunk,
+                                                  uint32_t* lds, uint32_t* __restrict__ out) {
+  const uint32_t P = 1u << lgP, K = lgP + 1, g = seg / K, b = seg - g * K;
+  const uint32_t cnt = b < lgP ? P / 2 : P;
+  Xyzz<F> v = xyzz_inf<F>();
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const uint32_t i = chunk * 2 * TREE_TPB + (uint32_t)h * TREE_TPB + threadIdx.x;
+    if (i < cnt) {
+      if (b < lgP) {
+        const uint32_t p = ((i >> b) << (b + 1)) | (1u << b) | (i & ((1u << b) - 1));
+        xyzz_add(v, load_xyzz<F>(s_in, (size_t)g * P + p));
+      } else {
+        xyzz_add(v, load_xyzz<F>(t_in, (size_t)g * P + i));
+      }
+    }
+  }
+  v = wg_tree_sum(v, lds);
+  if (threadIdx.x == 0) store_xyzz(out, (size_t)seg * nch + chunk, v);
+}
+
+// next tree level: segment seg of n_in values -> chunk sums out[seg * n_out + chunk]
+template <class F>
+__device__ __forceinline__ void subset_tree_next(const uint32_t* __restrict__ in, uint32_t n_in, uint32_t n_out,
+                                                 uint32_t seg, uint32_t chunk, uint32_t* lds,
+                                                 uint32_t* __restrict__ out) {
+  Xyzz<F> v = xyzz_inf<F>();
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const uint32_t i = chunk * 2 * TREE_TPB + (uint32_t)h * TREE_TPB + threadIdx.x;
+    if (i < n_in) xyzz_add(v, load_xyzz<F>(in, (size_t)seg * n_in + i));
+  }
+  v = wg_tree_sum(v, lds);
+  if (threadIdx.x == 0) store_xyzz(out, (size_t)seg * n_out + chunk, v);
 }
 
 }  // namespace msmk
