@@ -113,6 +113,16 @@ def main(n=300):
         wq = (wv << 261) // R
         lines.append("shoupr %s %s %s" % (l9(a, raw=k % 2 == 1), w8(wv), l9(wq)))
         checks.append(("shoupr", lambda z, a=a, wv=wv: z % R == a * wv % R and z < 3 * R))
+    # Shoup quotients of the NTT's stage roots (field.hpp shoup_quot) and sub4 against inputs < 4r
+    RP_ = 1 << 261
+    for wm in [0, 1, R - 1, R - 2] + [rnd.randrange(R) for _ in range(n)]:
+        w = wm * pow(RP_, -1, R) % R
+        lines.append("shoupq %s" % w8(wm))
+        checks.append(("shoupq", lambda z, w=w: z == (w << 261) // R))
+    for a in [0, 1, 3 * R - 1, 4 * R - 1, 2 * R] + [rnd.randrange(3 * R) for _ in range(n)]:
+        for b in [0, 4 * R, 3 * R - 1, rnd.randrange(3 * R)]:
+            lines.append("sub4r %s %s" % (w8(a), w8(b)))
+            checks.append(("sub4r", lambda z, a=a, b=b: z % R == (a - b) % R and z < 2 * R))
     # NTT radix-4 unit (field.hpp r4_dif): inputs and roots < 2m, incl. all-extreme operands
     r4 = [[rnd.randrange(2 * R) for _ in range(9)] for _ in range(n)]
     r4 += [[2 * R - 1] * 9, [0] * 9, [2 * R - 1, 0, 0, 2 * R - 1] + [2 * R - 1] * 5,
@@ -169,7 +179,12 @@ def main(n=300):
     out = subprocess.run([BIN], input="\n".join(lines) + "\n", capture_output=True, text=True).stdout.strip().split("\n")
     bad = {}
     for (name, fn), o in zip(checks, out):
-        v = int(o) if name == "iszq" else p8(o)
+        if name == "iszq":
+            v = int(o)
+        elif name == "shoupq":  # 9 limbs of 29 bits
+            v = sum(int(t, 16) << (29 * i) for i, t in enumerate(o.split()[:9]))
+        else:
+            v = p8(o)
         if not fn(v):
             bad[name] = bad.get(name, 0) + 1
     print("checked", len(checks), "bad", bad)

@@ -46,6 +46,12 @@ int main() {
       Fr a = rdl<FrCfg>(), w = rdf<FrCfg>(), wq = rdl<FrCfg>();
       prf(mul_shoup(a, w, wq));
     }
+    else if (o == "shoupq") {  // canonical Montgomery wm (words): Shoup quotient as 9 hex limbs
+      Fr wm = rdf<FrCfg>();
+      Fr q = shoup_quot(wm);
+      for (int i = 0; i < NL; ++i) printf("%08x ", q.v[i]);
+    }
+    else if (o == "sub4r") { Fr a = rdf<FrCfg>(), b = rdf<FrCfg>(); prf(sub4(a, b)); }
     else if (o == "r4d") {  // NTT radix-4 unit r4_dif: prints y0, y1, y2, y3
       Fr x0 = rdf<FrCfg>(), x1 = rdf<FrCfg>(), x2 = rdf<FrCfg>(), x3 = rdf<FrCfg>();
       Fr wa = rdf<FrCfg>(), wb = rdf<FrCfg>(), wc = rdf<FrCfg>(), wd = rdf<FrCfg>(), wj = rdf<FrCfg>();

@@ -25,6 +25,13 @@ def main(path, idx=2):
         cur += d
         last = t
     print("proof span %.2f ms, covered by saturating kernels %.2f ms" % ((t1 - t0) / 1e6, cov / 1e6))
+    # GPU idle at the proof boundary: last kernel end of this proof -> first kernel of the next
+    last_end = max(e for s, e, k in rows)
+    print("last kernel of the proof ends at %.2f ms; GPU idle until the next proof's first kernel: %.2f ms"
+          % (last_end / 1e6, (t1 - t0 - last_end) / 1e6))
+    tail = sorted([(s, e, k) for s, e, k in rows if s >= last_end - 2e6], key=lambda x: x[0])
+    for s, e, k in tail[-12:]:
+        print("  tail %8.2f %8.2f %7.3f %s" % (s / 1e6, e / 1e6, (e - s) / 1e6, k))
 
 
 if __name__ == "__main__":

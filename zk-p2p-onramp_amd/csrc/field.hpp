@@ -125,6 +125,30 @@ ZDEV Fe<C> mul_shoup(const Fe<C>& a, const Fe<C>& w, const Fe<C>& wq) {
   return r;
 }
 
+// Shoup quotient of a constant from its canonical Montgomery form wm = w 2^261 mod m (< m):
+// w 2^261 = wq m + wm, so wq = floor(w 2^261 / m) = -wm m^-1 mod 2^261 (a low-half product).
+template <class C>
+ZDEV Fe<C> shoup_quot(const Fe<C>& wm) {
+  uint32_t p[NL];
+  uint64_t acc = 0;
+#pragma unroll
+  for (int c = 0; c < NL; ++c) {
+#pragma unroll
+    for (int i = 0; i <= c; ++i) acc += (uint64_t)wm.v[i] * C::MINV261[c - i];
+    p[c] = (uint32_t)acc & LMASK;
+    acc >>= LB;
+  }
+  Fe<C> r;  // 2^261 - p  (mod 2^261)
+  uint32_t carry = 1;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) {
+    const uint32_t t = (LMASK - p[i]) + carry;
+    r.v[i] = t & LMASK;
+    carry = t >> LB;
+  }
+  return r;
+}
+
 // Montgomery product of a SUM of two products, (a*b + c*d)/2^261 mod m, with ONE
 // reduction ("lazy reduction"): the a*b, c*d and m*MOD partial products of a column
 // accumulate together.  All four operands normalised (limbs < 2^29; column sums
@@ -323,6 +347,21 @@ ZDEV Fe<C> sub(const Fe<C>& a, const Fe<C>& b) {
 #pragma unroll
   for (int i = 0; i < NL; ++i) s.v[i] = a.v[i] + C::MOD2_BORROW[i] - b.v[i];
   return reduce2(s);
+}
+
+// a - b for a normalised a < 4m and b <= 4m (computes a + 4m - b): output < 2m (Fr: qreduce < 1.2m).
+// The NTT with Shoup root products (outputs < 3m) subtracts with it.
+template <class C>
+ZDEV Fe<C> sub4(const Fe<C>& a, const Fe<C>& b) {
+  Fe<C> s;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) s.v[i] = a.v[i] + C::MOD4_BORROW[i] - b.v[i];
+  if constexpr (C::QRED) {
+    return qreduce(s);
+  } else {
+    normalize(s);
+    return cond_sub(cond_sub(s, C::MOD4), C::MOD2);
+  }
 }
 
 // ---- lazy subtractions: results that only ever feed a multiplication skip the final

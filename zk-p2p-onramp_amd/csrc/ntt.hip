@@ -28,8 +28,17 @@ constexpr int MAX_PASS_BITS = 8;
 #ifndef ZKP_NTT_WPE
 #define ZKP_NTT_WPE 0
 #endif
+// ZKP_NTT_SHOUP = 1: the stage-root products of the LDS stages are Shoup products by constants
+// (field.hpp mul_shoup: 143 mads, no per-column quotient digits) with each root's quotient staged
+// beside it in LDS; their outputs are < 3m, so the differences that take them use sub4.
+#ifndef ZKP_NTT_SHOUP
+#define ZKP_NTT_SHOUP 1
+#endif
+#if ZKP_NTT_SHOUP && (ZKP_NTT_MUL2 || ZKP_NTT_PACKED)
+#error "ZKP_NTT_SHOUP needs the four-multiply unit with unpacked roots"
+#endif
 constexpr int MAX_TW = ZKP_NTT_MUL2 ? (1 << MAX_PASS_BITS) : (1 << (MAX_PASS_BITS - 1));  // stage roots, b <= 8
-constexpr int RW = ZKP_NTT_PACKED ? 8 : NL;  // LDS words per root
+constexpr int RW = ZKP_NTT_SHOUP ? 2 * NL : (ZKP_NTT_PACKED ? 8 : NL);  // LDS words per root
 
 __device__ __forceinline__ uint32_t brev(uint32_t x, int b) { return __builtin_bitreverse32(x) >> (32 - b); }
 
@@ -64,9 +73,19 @@ __device__ __forceinline__ void put_root(uint32_t* __restrict__ ltw, int j, cons
 __device__ __forceinline__ void stage_roots(uint32_t* __restrict__ ltw, const uint32_t* __restrict__ loc, int b) {
   const int TW = 1 << (b - 1);
   for (int j = threadIdx.x; j < TW; j += TPB) {
-    const Fr x = load_fe<FrCfg>(loc + (size_t)(j << (LOC_LOG - b)) * 8);
+    const Fr x = load_fe<FrCfg>(loc + (size_t)(j << (LOC_LOG - b)) * 8);  // canonical Montgomery form
+#if ZKP_NTT_SHOUP
+    // plain root w (limbs 0..8) and its Shoup quotient floor(w 2^261 / r) (limbs 9..17)
+    const Fr w = from_mont(x), wq = shoup_quot(x);
+#pragma unroll
+    for (int l = 0; l < NL; ++l) {
+      ltw[l * MAX_TW + j] = w.v[l];
+      ltw[(NL + l) * MAX_TW + j] = wq.v[l];
+    }
+#else
     put_root(ltw, j, x);
     if (ZKP_NTT_MUL2) put_root(ltw, j + TW, neg(x));
+#endif
   }
 }
 
@@ -105,9 +124,25 @@ __device__ __forceinline__ Fr root(const uint32_t* __restrict__ ltw, uint32_t j)
   return w;
 #endif
 }
+// a * w_j for a stage root: a Shoup product (output < 3m) or a Montgomery one (< 2m)
+__device__ __forceinline__ Fr root_mul(const Fr& a, const uint32_t* __restrict__ ltw, uint32_t j) {
+#if ZKP_NTT_SHOUP
+  Fr w, wq;
+#pragma unroll
+  for (int l = 0; l < NL; ++l) {
+    w.v[l] = ltw[l * MAX_TW + j];
+    wq.v[l] = ltw[(NL + l) * MAX_TW + j];
+  }
+  return mul_shoup(a, w, wq);
+#else
+  return mul(a, root(ltw, j));
+#endif
+}
+// x - y for stage values (< 3m with Shoup products, else < 2m)
+__device__ __forceinline__ Fr stage_sub(const Fr& x, const Fr& y) { return ZKP_NTT_SHOUP ? sub4(x, y) : sub(x, y); }
 // DIF butterfly output d = (x - y) w_j, with w_0 = 1 (x - y only feeds the multiply: raw)
 __device__ __forceinline__ Fr bfly_d(const Fr& x, const Fr& y, const uint32_t* __restrict__ ltw, uint32_t j) {
-  return j ? mul(rsub(x, y), root(ltw, j)) : sub(x, y);
+  return j ? root_mul(rsub(x, y), ltw, j) : stage_sub(x, y);
 }
 // b radix-2 DIF stages on the LDS tile (rows natural in, bit-reversed out), done two at a
 // time as radix-4 groups in registers (half the LDS traffic and barriers of radix-2):
@@ -161,7 +196,7 @@ __device__ __forceinline__ void dft_stages(uint32_t* __restrict__ lds, const uin
       if (Hh > 1) {  // the sums stay raw (< 4m) and meet one reduction; w_H^0 = 1 (Montgomery) for i = 0
         const Fr s02 = add_raw(x0, x2), s13 = add_raw(x1, x3);
         lds_put(lds, E, p0, add_raw_reduce(s02, s13));
-        lds_put(lds, E, p1, mul(sub_raw6(s02, s13), root(ltw, j)));
+        lds_put(lds, E, p1, root_mul(sub_raw6(s02, s13), ltw, j));
       } else {  // last pair (span 1): no multiply in stage t+1
         const Fr s02 = add(x0, x2), s13 = add(x1, x3);
         lds_put(lds, E, p0, add(s02, s13));
@@ -180,7 +215,7 @@ __device__ __forceinline__ void dft_stages(uint32_t* __restrict__ lds, const uin
       const int p0 = swz((int)(bl << (b + lc)) + (int)((bq << 1) << lc) + (int)col), p1 = p0 ^ swz((int)C);
       const Fr x = lds_get(lds, E, p0), y = lds_get(lds, E, p1);
       lds_put(lds, E, p0, add(x, y));
-      lds_put(lds, E, p1, sub(x, y));  // span 1: the root is w_2^0 = 1
+      lds_put(lds, E, p1, stage_sub(x, y));  // span 1: the root is w_2^0 = 1
     }
     __syncthreads();
   }

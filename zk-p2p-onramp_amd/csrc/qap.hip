@@ -58,8 +58,9 @@ __global__ __launch_bounds__(TPB) void k_join_abc(const uint32_t* __restrict__ a
                                                   uint32_t* __restrict__ p) {
   const uint32_t j = blockIdx.x * TPB + threadIdx.x;
   if (j >= n) return;
-  Fr x = sub(mul(load_fe<FrCfg>(a + (size_t)j * 8), load_fe<FrCfg>(b + (size_t)j * 8)),
-             load_fe<FrCfg>(c + (size_t)j * 8));
+  // coset evaluations from the NTT are < 3m (Shoup stage products): a - c as a + 4m - c
+  Fr x = sub4(mul(load_fe<FrCfg>(a + (size_t)j * 8), load_fe<FrCfg>(b + (size_t)j * 8)),
+              load_fe<FrCfg>(c + (size_t)j * 8));
   store_fe(p + (size_t)j * 8, from_mont(x));
 }
 
