@@ -1,6 +1,8 @@
 // Groth16 prover core (see prover.hpp).
 #include "prover.hpp"
 
+#include <functional>
+
 #include <sys/random.h>
 
 #include <algorithm>
@@ -460,6 +462,8 @@ class DevicePipeline {
     Jac<HFq2> b2;
     float ms[6];
   };
+  // called with a, b1, c, b2 folded (h not yet) while the H MSM still runs on the device
+  using EarlyFn = std::function<void(const MsmOut&)>;
 
   // ---- witness upload slots.  acquire_upload() blocks until one of the NUP slots is free;
   // upload() copies a witness into it on the slot's stream (pageable H2D, the calling thread
@@ -504,13 +508,13 @@ class DevicePipeline {
     HIPX(hipEventElapsedTime(&ms, upev_[k][0], upev_[k][1]));
     return ms;
   }
-  MsmOut prove_uploaded(int k, float h2d_ms) {
+  MsmOut prove_uploaded(int k, float h2d_ms, const EarlyFn& early = {}) {
     std::lock_guard<std::mutex> lk(mu_);
     HIPX(hipSetDevice(dev_));
     maybe_inject_fault();
     HIPX(hipEventRecord(ev_[0], s0_));
     HIPX(hipEventRecord(ev_[1], s0_));
-    MsmOut o = prove_dev(up_[k]);
+    MsmOut o = prove_dev(up_[k], early);
     o.ms[0] = h2d_ms;
     return o;
   }
@@ -619,23 +623,23 @@ class DevicePipeline {
     }
   }
 
-  MsmOut prove(const WtnsView& w) {
+  MsmOut prove(const WtnsView& w, const EarlyFn& early = {}) {
     UploadSlot slot(this);
     const float ms = upload(slot.k, w);
-    return prove_uploaded(slot.k, ms);
+    return prove_uploaded(slot.k, ms, early);
   }
 
-  MsmOut prove_staged(int slot) {
+  MsmOut prove_staged(int slot, const EarlyFn& early = {}) {
     std::lock_guard<std::mutex> lk(mu_);
     HIPX(hipSetDevice(dev_));
     const uint32_t* d = slot_ptr(slot);
     HIPX(hipEventRecord(ev_[0], s0_));
     HIPX(hipEventRecord(ev_[1], s0_));
-    return prove_dev(d);
+    return prove_dev(d, early);
   }
 
   // the whole device pipeline on a resident witness (caller holds mu_, ev_[0..1] recorded)
-  MsmOut prove_dev(const uint32_t* d_wit) {
+  MsmOut prove_dev(const uint32_t* d_wit, const EarlyFn& early = {}) {
     // group-sum layout in dwin_: A | B1 | C (engines g1w_) | H (g1h) | B2 (g2)
     uint32_t* wa = dwin_;
     uint32_t* wh = dwin_ + 3 * wina_;
@@ -780,22 +784,40 @@ class DevicePipeline {
         std::rethrow_exception(e);
       }
     HIPX(hipEventRecord(ev_[4], s0_));
-    HIPX(hipStreamWaitEvent(s0_, ev_[6], 0));
-    HIPX(hipStreamWaitEvent(s0_, ev_[8], 0));
-    HIPX(hipMemcpyAsync(hwin_, dwin_, win_total() * 4, hipMemcpyDeviceToHost, s0_));
+    // the witness MSMs' group sums (A | B1 | C, B2) go to the host as soon as their finishes end
+    // (s3 holds the G1 finishes; it waits for the G2 finish), so the host folds them and the caller
+    // blinds A, B and the r/s part of C (`early`) while the H MSM still runs; only C + H, the
+    // affine conversions and the H fold remain after the device is done
+    HIPX(hipStreamWaitEvent(s3_, ev_[6], 0));
+    HIPX(hipMemcpyAsync(hwin_, dwin_, 3 * wina_ * 4, hipMemcpyDeviceToHost, s3_));
+    HIPX(hipMemcpyAsync(hwin_ + 3 * wina_ + winh_, wb2, (win_total() - 3 * wina_ - winh_) * 4, hipMemcpyDeviceToHost,
+                        s3_));
+    HIPX(hipEventRecord(ev_[15], s3_));
+    HIPX(hipMemcpyAsync(hwin_ + 3 * wina_, wh, winh_ * 4, hipMemcpyDeviceToHost, s0_));
     HIPX(hipEventRecord(ev_[5], s0_));
-    HIPX(hipStreamSynchronize(s0_));
-    for (auto& g : g1w_) g->collect(stats_g1_);
-    g1h_->collect(stats_g1_);
-    g2_->collect(stats_g2_);
     MsmOut o;
     const MsmParams& pa = g1w_[0]->params();
     const MsmParams& ph = g1h_->params();
+    HIPX(hipEventSynchronize(ev_[15]));
     o.a = msm_fold<HFq>(hwin_, pa);
     o.b1 = msm_fold<HFq>(hwin_ + wina_, pa);
     o.c = msm_fold<HFq>(hwin_ + 2 * wina_, pa);
-    o.h = msm_fold<HFq>(hwin_ + 3 * wina_, ph);
     o.b2 = msm_fold<HFq2>(hwin_ + 3 * wina_ + winh_, pa);
+    if (early) {
+      try {
+        early(o);
+      } catch (...) {
+        (void)hipStreamSynchronize(s0_);  // the H MSM and its copy still run: drain before rethrowing
+        (void)hipStreamSynchronize(s3_);
+        throw;
+      }
+    }
+    HIPX(hipStreamSynchronize(s0_));
+    HIPX(hipStreamSynchronize(s3_));
+    for (auto& g : g1w_) g->collect(stats_g1_);
+    g1h_->collect(stats_g1_);
+    g2_->collect(stats_g2_);
+    o.h = msm_fold<HFq>(hwin_ + 3 * wina_, ph);
     HIPX(hipEventElapsedTime(&o.ms[0], ev_[0], ev_[1]));  // wtns H2D
     HIPX(hipEventElapsedTime(&o.ms[1], ev_[1], ev_[2]));  // buildABC
     HIPX(hipEventElapsedTime(&o.ms[2], ev_[2], ev_[3]));  // NTT + join
@@ -885,27 +907,38 @@ DevicePipeline& Prover::pick_device() {
 
 Prover::~Prover() = default;
 
-static void assemble(const ZkeyHeader& h, const DevicePipeline::MsmOut& m, const WtnsView& w, const uint8_t* r32,
-                     const uint8_t* s32, zkp_proof* out) {
+// snarkjs groth16_prove's blinding, in two phases: everything but piH
+// (assemble_pre: runs while the H MSM is still on the device) and C + piH + the encoding.
+struct Blinded {
+  Jac<HFq> A, Cpart;  // Cpart = piC' + s A + r B1 - (r s) delta1
+  Jac<HFq2> B;
+};
+static Blinded assemble_pre(const ZkeyHeader& h, const DevicePipeline::MsmOut& m, const uint8_t* r32,
+                            const uint8_t* s32) {
   const U256 r = scalar_or_random(r32), s = scalar_or_random(s32);
   const Jac<HFq> alpha1 = host::jac_from_aff(h.alpha1), beta1 = host::jac_from_aff(h.beta1),
                  delta1 = host::jac_from_aff(h.delta1);
   const Jac<HFq2> beta2 = host::jac_from_aff(h.beta2), delta2 = host::jac_from_aff(h.delta2);
+  Blinded o;
   // A = piA' + alpha1 + r delta1
-  Jac<HFq> A = host::jac_add(host::jac_add(m.a, alpha1), host::jac_mul(delta1, r));
+  o.A = host::jac_add(host::jac_add(m.a, alpha1), host::jac_mul(delta1, r));
   // B = piB' + beta2 + s delta2 ; B1 = piB1' + beta1 + s delta1
-  Jac<HFq2> B = host::jac_add(host::jac_add(m.b2, beta2), host::jac_mul(delta2, s));
+  o.B = host::jac_add(host::jac_add(m.b2, beta2), host::jac_mul(delta2, s));
   Jac<HFq> B1 = host::jac_add(host::jac_add(m.b1, beta1), host::jac_mul(delta1, s));
   // C = piC' + piH + s A + r B1 - (r s) delta1
   HFr rs = HFr::from_std(r) * HFr::from_std(s);
   U256 nrs = rs.neg().to_std();
-  Jac<HFq> C = host::jac_add(m.c, m.h);
-  C = host::jac_add(C, host::jac_mul(A, s));
+  Jac<HFq> C = m.c;
+  C = host::jac_add(C, host::jac_mul(o.A, s));
   C = host::jac_add(C, host::jac_mul(B1, r));
-  C = host::jac_add(C, host::jac_mul(delta1, nrs));
-  auto a = host::jac_to_aff(A);
-  auto b = host::jac_to_aff(B);
-  auto c = host::jac_to_aff(C);
+  o.Cpart = host::jac_add(C, host::jac_mul(delta1, nrs));
+  return o;
+}
+static void assemble_post(const ZkeyHeader& h, const Blinded& bl, const Jac<HFq>& piH, const WtnsView& w,
+                          zkp_proof* out) {
+  auto a = host::jac_to_aff(bl.A);
+  auto b = host::jac_to_aff(bl.B);
+  auto c = host::jac_to_aff(host::jac_add(bl.Cpart, piH));
   put_fq(a.x, out->pi_a[0]);
   put_fq(a.y, out->pi_a[1]);
   put_fq(b.x.c0, out->pi_b[0][0]);
@@ -917,6 +950,10 @@ static void assemble(const ZkeyHeader& h, const DevicePipeline::MsmOut& m, const
   out->n_public = h.n_public;
   if (out->public_signals && out->public_capacity)
     std::memcpy(out->public_signals, w.values + 32, (size_t)std::min(h.n_public, out->public_capacity) * 32);
+}
+static void assemble(const ZkeyHeader& h, const DevicePipeline::MsmOut& m, const WtnsView& w, const uint8_t* r32,
+                     const uint8_t* s32, zkp_proof* out) {
+  assemble_post(h, assemble_pre(h, m, r32, s32), m.h, w, out);
 }
 
 static WtnsView check_wtns(const ZkeyHeader& h, const uint8_t* wtns, size_t len) {
@@ -1030,14 +1067,15 @@ void Prover::prove(const uint8_t* wtns, size_t len, const uint8_t* r32, const ui
   WtnsView w = check_wtns(hdr_, wtns, len);
   DevicePipeline& d = pick_device();
   DevicePipeline::MsmOut m;
+  Blinded bl;
   try {
-    m = d.prove(w);
+    m = d.prove(w, [&](const DevicePipeline::MsmOut& o) { bl = assemble_pre(hdr_, o, r32, s32); });
   } catch (const HipError&) {
     d.mark_failed();
     throw;
   }
   auto t1 = std::chrono::steady_clock::now();
-  assemble(hdr_, m, w, r32, s32, out);
+  assemble_post(hdr_, bl, m.h, w, out);
   auto t2 = std::chrono::steady_clock::now();
   std::lock_guard<std::mutex> lk(tmu_);
   for (int i = 0; i < 5; ++i) last_ms_[i] = m.ms[i];
@@ -1095,8 +1133,11 @@ zkp_status Prover::prove_batch(const uint8_t* const* wtns, const size_t* lens, i
         continue;
       }
       try {
-        DevicePipeline::MsmOut m = d.prove(w);
-        assemble(hdr_, m, w, r32s ? r32s[i] : nullptr, s32s ? s32s[i] : nullptr, &outs[i]);
+        Blinded bl;
+        DevicePipeline::MsmOut m = d.prove(w, [&](const DevicePipeline::MsmOut& o) {
+          bl = assemble_pre(hdr_, o, r32s ? r32s[i] : nullptr, s32s ? s32s[i] : nullptr);
+        });
+        assemble_post(hdr_, bl, m.h, w, &outs[i]);
         finish(i, ZKP_OK, "");
       } catch (const HipError& e) {
         d.mark_failed();
@@ -1169,7 +1210,9 @@ void Prover::prove_staged(int dev, int slot, const uint8_t* r32, const uint8_t* 
   require_full();
   if (dev < 0 || dev >= (int)devs_.size()) throw ZkpError(ZKP_ERR_INVALID_ARG, "device index out of range");
   auto t0 = std::chrono::steady_clock::now();
-  DevicePipeline::MsmOut m = devs_[dev]->prove_staged(slot);
+  Blinded bl;
+  DevicePipeline::MsmOut m = devs_[dev]->prove_staged(
+      slot, [&](const DevicePipeline::MsmOut& o) { bl = assemble_pre(hdr_, o, r32, s32); });
   auto t1 = std::chrono::steady_clock::now();
   WtnsView w;
   {
@@ -1177,7 +1220,7 @@ void Prover::prove_staged(int dev, int slot, const uint8_t* r32, const uint8_t* 
     w.values = staged_pub_[dev][slot].data();
     w.n_witness = hdr_.n_vars;
   }
-  assemble(hdr_, m, w, r32, s32, out);
+  assemble_post(hdr_, bl, m.h, w, out);
   auto t2 = std::chrono::steady_clock::now();
   std::lock_guard<std::mutex> lk(tmu_);
   for (int i = 0; i < 5; ++i) last_ms_[i] = m.ms[i];
