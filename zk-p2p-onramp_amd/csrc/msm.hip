@@ -462,10 +462,12 @@ void run_finish(const MsmPlan& plan, uint32_t* part_a, uint32_t* part_b, uint32_
     if ((size_t)G * K * n <= tree_first_max()) {  // about one round of workgroups: the tree from the inputs
       hipLaunchKernelGGL(k_subset_tree_first<F>, dim3(n, G * K), dim3(msmk::TREE_TPB), 0, st, seg_s, seg_t, lgP, n,
                          sub[0]);
-    } else {  // many inputs (the H MSM: K x 2^16): full-lane fan-in chains first, trees above them
-      n = (((1u << lgP) + 2 * fan - 1) / (2 * fan));
+    } else {  // many inputs (the H MSM: K x 2^16): full-lane fan-in chains first (short: the trees
+              // above them take the rest), then trees
+      const uint32_t cf = std::min<uint32_t>(fan, msmk::TREE_CHAIN_FAN);
+      n = (((1u << lgP) + 2 * cf - 1) / (2 * cf));
       hipLaunchKernelGGL(k_subset_first<F>, dim3(grid_for((size_t)G * K * n)), dim3(TPB), 0, st, seg_s, seg_t, G,
-                         lgP, fan, sub[0]);
+                         lgP, cf, sub[0]);
     }
     while (n > 1) {
       const uint32_t next = (n + CH - 1) / CH;
@@ -806,7 +808,8 @@ MsmEngine::MsmEngine(Curve curve, const MsmParams& prm, size_t max_n, hipStream_
   HIPX(hipMalloc(&seg_s_, nseg * xyzz_words * 4));
   HIPX(hipMalloc(&seg_t_, nseg * xyzz_words * 4));
   const size_t n1 = (size_t)prm_.groups * prm_.K() *
-                    std::max(((half / prm_.M) + 2 * prm_.L - 1) / (2 * prm_.L),
+                    std::max(((half / prm_.M) + 2 * std::min<size_t>(prm_.L, msmk::TREE_CHAIN_FAN) - 1) /
+                                 (2 * std::min<size_t>(prm_.L, msmk::TREE_CHAIN_FAN)),
                              ((half / prm_.M) + 2 * msmk::TREE_TPB - 1) / (2 * msmk::TREE_TPB));
   for (int i = 0; i < 2; ++i) HIPX(hipMalloc(&sub_[i], n1 * xyzz_words * 4));
   for (auto& e : ev_) {

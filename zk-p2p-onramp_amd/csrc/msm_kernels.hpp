@@ -113,6 +113,10 @@ ZDEV uint32_t task_len(uint32_t t, const uint32_t* __restrict__ start, const uin
   return umin(end[b], s0 + S) - s0;
 }
 
+#ifndef ZKP_ACC_VALS_AHEAD
+#define ZKP_ACC_VALS_AHEAD 1
+#endif
+
 // thread i runs task perm[i] (tasks ordered by length, longest first: the lanes of a wave run
 // equally long chains) or task i (perm == nullptr)
 template <class F>
@@ -133,8 +137,17 @@ ZDEV void accumulate(uint32_t i, const uint32_t* __restrict__ points, const uint
                              load_aff<F>(points, v1 & 0x7fffffffu), (v1 >> 31) != 0);
     j = s0 + 2;
   }
+#if ZKP_ACC_VALS_AHEAD
+  // the next entry's index is loaded one addition ahead: each iteration then waits on one
+  // memory latency (its base gather) instead of two dependent ones (index, then base)
+  uint32_t vn = j < s1 ? vals[j] : 0u;
+  for (; j < s1; ++j) {
+    const uint32_t v = vn;
+    if (j + 1 < s1) vn = vals[j + 1];
+#else
   for (; j < s1; ++j) {
     const uint32_t v = vals[j];
+#endif
 #ifdef ZKP_ACC_GATHER_MASK  // latency probe only (wrong results): gathers confined to a cache-resident slice
     xyzz_add_aff(acc, load_aff<F>(points, v & ZKP_ACC_GATHER_MASK), (v >> 31) != 0);
 #else
@@ -276,6 +289,7 @@ ZDEV void subset_level(uint32_t id, const uint32_t* __restrict__ in, uint32_t ns
 // fan-in-L chains over ceil(log_L(P/2)) dependent launches (the finish is latency-bound: every
 // sequential full addition costs ~5 us on a lightly loaded SIMD).
 constexpr int TREE_TPB = 256;
+constexpr uint32_t TREE_CHAIN_FAN = 4;  // fan-in of the chain level below the trees (large subset sums)
 template <class F>
 struct XyzzLimbs;  // 32-bit words of one XYZZ point in the 9-limb compute form
 template <>
