@@ -131,6 +131,12 @@ def test_msm_dense_counting_sort_large(monkeypatch):
     monkeypatch.setenv("ZKP_MSM_DENSE", "1")
     assert zkp_amd.msm_g1(pb, sb, window_bits=20) == want
     assert zkp_amd.msm_g1(pb, sb, window_bits=13) == want
+    # the subset sums (c = 20: 18 sums of 2^16 values) with a chain level below the trees (default
+    # above 512 workgroups), from the inputs by trees (two tree levels), and by the launch chain
+    monkeypatch.setenv("ZKP_TREE_FIRST_MAX", "100000")
+    assert zkp_amd.msm_g1(pb, sb, window_bits=20) == want
+    monkeypatch.setenv("ZKP_SUBSET_TREE", "0")
+    assert zkp_amd.msm_g1(pb, sb, window_bits=20) == want
     # the oracle on the same sum: scalars of equal bases add up
     acc = [0] * 64
     for i, x in enumerate(sc):

@@ -35,9 +35,11 @@ def test_prove_bit_exact(golden_dir, name):
 # plan / reduction / scheduling variants (read when the prover is built): the compacted H plan
 # instead of the dense one, the dense plan on the rocprim radix sort instead of the hand-written
 # counting sort, other bucket-reduction segment sizes and fan-ins, and the
-# scheduling gates -- every variant must give the same golden proof
+# scheduling gates, the subset sums by launch chains or with a chain level below the trees --
+# every variant must give the same golden proof
 KNOBS = [{"ZKP_H_DENSE": "0"}, {"ZKP_H_SORT": "rocprim"}, {"ZKP_TASK_ORDER": "bucket"}, {"ZKP_SEG_M": "16", "ZKP_SUB_L": "4"}, {"ZKP_SEG_M": "2", "ZKP_SUB_L": "16"},
-         {"ZKP_SCHED": "4"}, {"ZKP_SCHED": "5"}, {"ZKP_G2_FINISH_GATE": "1"}, {"ZKP_G2_FINISH_GATE": "2"}]
+         {"ZKP_SCHED": "4"}, {"ZKP_SCHED": "5"}, {"ZKP_G2_FINISH_GATE": "1"}, {"ZKP_G2_FINISH_GATE": "2"},
+         {"ZKP_SUBSET_TREE": "0"}, {"ZKP_TREE_FIRST_MAX": "0"}]
 
 
 @pytest.mark.parametrize("knobs", KNOBS, ids=lambda k: ",".join("%s=%s" % kv for kv in k.items()))

@@ -216,19 +216,14 @@ __global__ __launch_bounds__(msmk::TREE_TPB) void k_subset_tree_next(
 }
 // largest first-level tree grid (workgroups); larger subset sums (the proof's MSMs) start with
 // full-lane fan-in chains (ZKP_TREE_FIRST_MAX overrides)
+// (read per finish, so tests can switch them per prover)
 static size_t tree_first_max() {
-  static const size_t v = [] {
-    const char* e = std::getenv("ZKP_TREE_FIRST_MAX");
-    return e ? (size_t)std::atol(e) : (size_t)512;
-  }();
-  return v;
+  const char* e = std::getenv("ZKP_TREE_FIRST_MAX");
+  return e ? (size_t)std::atol(e) : (size_t)512;
 }
 static bool subset_tree() {
-  static const bool on = [] {
-    const char* e = std::getenv("ZKP_SUBSET_TREE");
-    return !(e && std::atoi(e) == 0);
-  }();
-  return on;
+  const char* e = std::getenv("ZKP_SUBSET_TREE");
+  return !(e && std::atoi(e) == 0);
 }
 
 // Bucket-key sort: rocprim onesweep with 9-bit digits (512-way, 2 passes for the 17/18-bit keys

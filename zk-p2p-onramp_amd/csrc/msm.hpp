@@ -115,7 +115,8 @@ class MsmPlan {
   ~MsmPlan();
   MsmPlan(const MsmPlan&) = delete;
   MsmPlan& operator=(const MsmPlan&) = delete;
-  // scalars: device, 8 LE 32-bit words each (standard form, any value < 2^256).
+  // scalars: device, 8 LE 32-bit words each (standard form, any value < 2^256: reduced below r
+  // when loaded, msm_kernels.hpp load_scalar, so W = ceil(255 / c) windows always hold the carry).
   // Enqueues on the plan's stream and blocks the host once (the task grid needs the
   // number of nonzero digits); records ready() at the end.  Grouping by bucket: a stable
   // rocprim radix sort, or with ZKP_PLAN_SORT=bins a two-level counting sort (msm.hip).

@@ -321,6 +321,54 @@ static void split_range(size_t n, int part, int nparts, size_t& lo, size_t& hi) 
   hi = n * (size_t)(part + 1) / (size_t)nparts;
 }
 
+// A long-lived host thread that runs one job at a time (the per-proof G1 / G2 enqueue jobs of a
+// pipeline: no thread creation on the proof's critical path)
+class JobThread {
+ public:
+  JobThread() : th_([this] { loop(); }) {}
+  ~JobThread() {
+    {
+      std::lock_guard<std::mutex> lk(m_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    th_.join();
+  }
+  void start(std::function<void()> f) {
+    {
+      std::lock_guard<std::mutex> lk(m_);
+      job_ = std::move(f);
+      done_ = false;
+    }
+    cv_.notify_all();
+  }
+  void wait() {
+    std::unique_lock<std::mutex> lk(m_);
+    cv_.wait(lk, [&] { return done_; });
+  }
+
+ private:
+  void loop() {
+    std::unique_lock<std::mutex> lk(m_);
+    for (;;) {
+      cv_.wait(lk, [&] { return stop_ || job_; });
+      if (!job_) return;  // stop with no job pending
+      std::function<void()> f = std::move(job_);
+      job_ = nullptr;
+      lk.unlock();
+      f();  // the jobs catch their own exceptions
+      lk.lock();
+      done_ = true;
+      cv_.notify_all();
+    }
+  }
+  std::mutex m_;
+  std::condition_variable cv_;
+  std::function<void()> job_;
+  bool stop_ = false, done_ = true;
+  std::thread th_;  // last: started once the state above exists
+};
+
 class DevicePipeline {
  public:
   // part / nparts: this pipeline holds only slice `part` of every point section (the
@@ -773,10 +821,11 @@ class DevicePipeline {
       if (!err[0]) g2_job();
       if (!err[0] && !err[1]) h_job();
     } else {
-      std::thread t_g2(g2_job), t_g1(g1_job);
+      jt_g2_.start(g2_job);
+      jt_g1_.start(g1_job);
       h_job();
-      t_g1.join();
-      t_g2.join();
+      jt_g1_.wait();
+      jt_g2_.wait();
     }
     for (auto& e : err)
       if (e) {
@@ -838,6 +887,7 @@ class DevicePipeline {
   hipStream_t s0_ = nullptr, s1_ = nullptr, s2_ = nullptr, s3_ = nullptr;
   hipStream_t s4_ = nullptr;  // H plan on the reserved CUs (ZKP_RESERVE_CUS > 0), else s0
   hipEvent_t ev_[16];
+  JobThread jt_g1_, jt_g2_;  // host threads feeding s2 (witness plan, G1 MSMs) and s1 (G2 MSM)
   std::unique_ptr<MsmBases> ta_, tb1_, tc_, tb2_, th_;
   uint32_t* rowptr_[2] = {nullptr, nullptr};
   uint32_t* col_[2] = {nullptr, nullptr};
