@@ -58,6 +58,18 @@ struct WtnsView {
 };
 WtnsView parse_wtns(const uint8_t* buf, size_t len);
 
+struct Csr {
+  std::vector<uint32_t> rowptr, col, val;  // val: 8 words per entry (raw zkey bytes)
+};
+// a groth16 zkey: sections, header (validated: curve, sizes of sections 4-9, power-of-two
+// domain <= 2^27) and, with_coefs, the A/B coefficients as CSR by (matrix, constraint)
+struct ZkeyParsed {
+  BinFile bf;
+  ZkeyHeader hdr;
+  Csr csr[2];
+};
+ZkeyParsed parse_zkey(const uint8_t* buf, size_t len, bool with_coefs = true);
+
 class DevicePipeline;
 
 class Prover {
