@@ -116,6 +116,28 @@ def test_msm_g1_dense_counting_sort(monkeypatch):
         assert zkp_amd.msm_g1(pb, sb, window_bits=c, table_depth=d) == groth16.msm_g1(p, [x % R for x in s]), (c, d)
 
 
+@pytest.mark.parametrize("c", [17, 18, 19, 21, 22])
+def test_msm_dense_window_bits(monkeypatch, c):
+    # the hand-written sort's bin / sub-bin / bucket bit splits of every window width around the
+    # prover's choices (c = 18: 6 + 6 + 5 bits, 19: 7 + 6 + 5, 21: 8 + 7 + 5 ...), 2^15 uniform
+    # scalars over 64 bases: dense plan == compacted plan == the oracle's sum
+    rng = circuit.SplitMix64(46, 1)
+    n = 1 << 15
+    g = bn254.FixedBase(bn254.G1_GEN)
+    base = [g.mul(rng.fr() or 1) for _ in range(64)]
+    pts = [base[i % 64] for i in range(n)]
+    sc = [rng.fr() for _ in range(n)]
+    pb, sb = _blob(pts, sc)
+    monkeypatch.setenv("ZKP_MSM_DENSE", "1")
+    got = zkp_amd.msm_g1(pb, sb, window_bits=c)
+    monkeypatch.setenv("ZKP_MSM_DENSE", "0")
+    assert zkp_amd.msm_g1(pb, sb, window_bits=c) == got
+    acc = [0] * 64
+    for i, x in enumerate(sc):
+        acc[i % 64] = (acc[i % 64] + x) % R
+    assert got == groth16.msm_g1(base, acc)
+
+
 def test_msm_dense_counting_sort_large(monkeypatch):
     # several scatter workgroups and every coarse bin populated: 2^14 uniform scalars at c = 20 on
     # the dense plan vs the compacted plan (rocprim sort) of the same input, G1 and G2

@@ -1,0 +1,14 @@
+# window bits re-sweep after the subset-sum trees (the bucket reduction got cheaper): witness and H plans
+set -e
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+rm -f gpurun_out/csweep.txt
+run() { tag="$*"; env "$@" timeout -k 10 300 python bench.py --steps 16 --warmup 3 --cpu-baseline none --batch 0 --no-kernels > gpurun_out/b_cs.log 2>&1; echo "$tag $(tail -1 gpurun_out/b_cs.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["ms_per_step"], d["config"]["msm"])')" >> gpurun_out/csweep.txt; }
+for i in 1 2; do
+  run ZKP_NONE=0
+  run ZKP_WINDOW_BITS_W=19
+  run ZKP_WINDOW_BITS_H=21
+  run ZKP_WINDOW_BITS_H=22
+done
+run ZKP_WINDOW_BITS_W=17
+run ZKP_NONE=0

@@ -76,6 +76,24 @@ struct MsmParams {
   size_t buckets() const { return (size_t)groups * half(); }
 };
 
+// Window bits for a DENSE plan (hand-written bucket sort) near c.  The top window of a 254-bit
+// scalar holds only 254 - (W - 1) c digit bits: for c = 18, 19, 21 (2, 7, 2 bits) all n of its
+// digits fall into a handful of buckets, i.e. into one or a few sub-bins of the sort's pass C,
+// which gives every sub-bin ONE workgroup -- measured 1.3 ms for that kernel alone at 2^20
+// points and c = 18 (0.05 ms at c = 20), +13 ms per Venmo proof at c = 21
+// (tools/gpu/experiments/r2_hsort_c*.sh).  Keep c whose top window spans >= 12 bits (>= 128
+// sub-bins), trying c+1, c-1, c+2, ... within [8, 20]; below 2^17 points one workgroup per
+// sub-bin copes (n entries at most), so c stays.
+inline int dense_window_bits(int c, size_t n) {
+  auto top = [](int cc) { return 254 - ((255 + cc - 1) / cc - 1) * cc; };
+  if (n < (size_t(1) << 17) || top(c) >= 12) return c;
+  for (int d = 1; d <= 6; ++d) {
+    if (c + d <= 20 && top(c + d) >= 12) return c + d;
+    if (c - d >= 8 && top(c - d) >= 12) return c - d;
+  }
+  return c;
+}
+
 // words per coordinate element: G1 -> Fq (8 words), G2 -> Fq2 (16 words)
 enum class Curve { G1 = 1, G2 = 2 };
 

@@ -115,7 +115,8 @@ static void choose_msm_params(size_t n_w, size_t n_h, MsmParams& pw, MsmParams& 
   auto clampc = [](int c) { return c < 8 ? 8 : (c > 20 ? 20 : c); };
   const int c = env_int("ZKP_WINDOW_BITS", 0), d = env_int("ZKP_TABLE_DEPTH", 0);
   const int cw = env_int("ZKP_WINDOW_BITS_W", c ? c : clampc(lg(n_w) - 5));
-  const int ch = env_int("ZKP_WINDOW_BITS_H", c ? c : clampc(lg(n_h) - 3));
+  // (the dense H plan avoids window widths whose top window collapses into a few buckets)
+  const int ch = env_int("ZKP_WINDOW_BITS_H", c ? c : dense_window_bits(clampc(lg(n_h) - 3), n_h));
   const int sw = env_int("ZKP_TASK_W", 0), sh = env_int("ZKP_TASK_H", 0);  // entries per task (tuning)
   // buckets per reduction segment / subset-sum fan-in (tuning; powers of two)
   const int sm = env_int("ZKP_SEG_M", 0), sl = env_int("ZKP_SUB_L", 0);
@@ -1168,7 +1169,7 @@ struct MsmRig {
       // c = lg n - 4.  ZKP_MSM_C / ZKP_MSM_DENSE=0 override (A/B).
       int lg = 0;
       while ((size_t(1) << lg) < n) ++lg;
-      const int c_auto = env_int("ZKP_MSM_C", std::min(20, std::max(8, lg - 3)));
+      const int c_auto = env_int("ZKP_MSM_C", dense_window_bits(std::min(20, std::max(8, lg - 3)), n));
       prm = MsmParams::make(std::max<size_t>(n, 1), c ? c : c_auto, depth);
       bases = std::make_unique<MsmBases>(curve, n, prm.c, prm.depth);
       fill_bases(*bases, points, n, 0, st);
