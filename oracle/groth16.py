@@ -88,12 +88,17 @@ def prove(z: ZKey, w, r: int, s: int):
     return {"A": A, "B": B, "C": C}, w[1:z.n_public + 1]
 
 
-def split_range(n: int, part: int, nparts: int):
-    """[lo, hi) of slice `part` of n items in nparts contiguous ranges (as prover.hip split_range)."""
-    return n * part // nparts, n * (part + 1) // nparts
+def split_range(n: int, part: int, nparts: int, balance: bool = False):
+    """[lo, hi) of slice `part` of n items in nparts contiguous ranges (as prover.hip split_range);
+    balance (ZKP_SPLIT_BALANCE=1 there): for nparts > 3, parts 0..2 (the quotient-vector owners)
+    weigh 3 and the others 8."""
+    if not balance or nparts <= 3:
+        return n * part // nparts, n * (part + 1) // nparts
+    cum = lambda k: 3 * min(k, 3) + 8 * max(k - 3, 0)  # noqa: E731
+    return n * cum(part) // cum(nparts), n * cum(part + 1) // cum(nparts)
 
 
-def partial_sums(z: ZKey, w, part: int, nparts: int, h=None):
+def partial_sums(z: ZKey, w, part: int, nparts: int, h=None, balance: bool = False):
     """MSM partial sums of point slice `part` of `nparts` (the point-range split of one proof,
     SURVEY.md §8e E1(2)): witness-indexed sections A, B1, B2, C over [wlo, whi) (C's base of
     signal i is z.c[i - nPublic - 1]), H over [hlo, hhi) of the domain.  Summing the partials
@@ -101,8 +106,8 @@ def partial_sums(z: ZKey, w, part: int, nparts: int, h=None):
     w = [x % R for x in w]
     if h is None:
         h = quotient_scalars(z, w)
-    wlo, whi = split_range(z.n_vars, part, nparts)
-    hlo, hhi = split_range(z.domain_size, part, nparts)
+    wlo, whi = split_range(z.n_vars, part, nparts, balance)
+    hlo, hhi = split_range(z.domain_size, part, nparts, balance)
     c0 = z.n_public + 1
     cidx = [i for i in range(max(wlo, c0), whi)]
     return {

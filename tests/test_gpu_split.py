@@ -34,13 +34,17 @@ def test_full_prover_partial_is_part_0_of_1():
     assert p.prove_raw(wt, r, s)[0] == (a, b, c)
 
 
-@pytest.mark.parametrize("name,nparts", [("small", 2), ("small", 3), ("venmo_mini", 4)])
-def test_split_distributed_quotient(name, nparts):
+@pytest.mark.parametrize("name,nparts,balance", [("small", 2, False), ("small", 3, False), ("venmo_mini", 4, False),
+                                                  ("venmo_mini", 5, True), ("small", 4, True)])
+def test_split_distributed_quotient(name, nparts, balance, monkeypatch):
     # the distributed quotient on one GPU: part v % nparts extends vector v only
     # (zkp_quotient_part_staged), every part joins just its domain slice from the exchanged
-    # slices (zkp_prove_partial_ext_staged); partials and proof stay bit-exact
+    # slices (zkp_prove_partial_ext_staged); partials and proof stay bit-exact.  balance:
+    # ZKP_SPLIT_BALANCE=1 weighted point slices (the quotient-vector owners take fewer points)
     import torch
     from zkp_amd.dist import split_range
+    if balance:
+        monkeypatch.setenv("ZKP_SPLIT_BALANCE", "1")
     zk, wt, r, s, want = _case(name)
     provers = [zkp_amd.Prover(zk, devices=[0], part=k, nparts=nparts) for k in range(nparts)]
     n = provers[0].domain_size
@@ -59,6 +63,6 @@ def test_split_distributed_quotient(name, nparts):
         parts.append(p.prove_partial_ext_staged(0, [t.data_ptr() for t in sl]))
     for p in provers:
         p.close()
-    assert parts == _oracle_partials(zk, wt, nparts)
+    assert parts == _oracle_partials(zk, wt, nparts, balance)
     (a, b, c), _ = zkp_amd.proof_combine_raw(zk, parts, wt, r, s)
     assert {"A": a, "B": b, "C": c} == want

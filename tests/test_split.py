@@ -28,13 +28,13 @@ def _case(name):
     return zk, wt, int(man["r"]), int(man["s"]), want
 
 
-def _oracle_partials(zk, wt, nparts):
+def _oracle_partials(zk, wt, nparts, balance=False):
     z = binfile.read_zkey(zk)
     w = binfile.read_wtns(wt)[1]
     h = groth16.quotient_scalars(z, [x % groth16.R for x in w])
     out = []
     for k in range(nparts):
-        p = groth16.partial_sums(z, w, k, nparts, h)
+        p = groth16.partial_sums(z, w, k, nparts, h, balance)
         out.append(zkp_amd.partial_from_points(p["a"], p["b1"], p["c"], p["h"], p["b2"], k, nparts))
     return out
 
@@ -97,10 +97,12 @@ def test_split_allgather_gloo_world2():
         assert {"A": a, "B": b, "C": c} == want
 
 
-def _xchg_worker(rank, world, port, n, q):
+def _xchg_worker(rank, world, port, n, q, balance=False):
     import torch
     import torch.distributed as dist
     from zkp_amd.dist import exchange_quotient_slices, split_range
+    if balance:
+        os.environ["ZKP_SPLIT_BALANCE"] = "1"
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -117,15 +119,15 @@ def _xchg_worker(rank, world, port, n, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,n", [(2, 64), (3, 50), (4, 37)])
-def test_distributed_quotient_exchange_gloo(world, n):
+@pytest.mark.parametrize("world,n,balance", [(2, 64, False), (3, 50, False), (4, 37, False), (5, 101, True)])
+def test_distributed_quotient_exchange_gloo(world, n, balance):
     # the slice exchange of the distributed quotient (zkp_amd.dist.exchange_quotient_slices,
     # RCCL point-to-point on GPUs): rank v % world owns vector v, every rank ends up with its
     # domain slice of all three, ragged slice sizes included
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_xchg_worker, args=(k, world, port, n, q)) for k in range(world)]
+    procs = [ctx.Process(target=_xchg_worker, args=(k, world, port, n, q, balance)) for k in range(world)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=300) for _ in procs)
@@ -171,3 +173,18 @@ def test_split_blinding_agreed_gloo_world2():
     zk, _, _, _, _ = _case("tiny")
     a, b, c = pr0
     assert groth16.verify_with_zkey(binfile.read_zkey(zk), pub0, {"A": a, "B": b, "C": c})
+
+
+@pytest.mark.parametrize("balance", [False, True])
+def test_split_ranges_agree(balance):
+    # zkp_amd.dist.split_range (the exchange, the emulation) and the oracle's (partial sums) give
+    # the same contiguous tiling of [0, n) -- the C++ split_range is checked against them through
+    # the GPU split tests; balanced: parts 0..2 weigh 3, the others 8 (nparts > 3)
+    from zkp_amd.dist import split_range
+    for n in (1, 7, 100, 1 << 21, 6_400_562):
+        for nparts in range(1, 10):
+            rs = [split_range(n, k, nparts, balance) for k in range(nparts)]
+            assert rs == [groth16.split_range(n, k, nparts, balance) for k in range(nparts)]
+            assert rs[0][0] == 0 and rs[-1][1] == n and all(rs[k][1] == rs[k + 1][0] for k in range(nparts - 1))
+            if balance and nparts > 3 and n >= 1 << 21:
+                assert (rs[0][1] - rs[0][0]) * 8 < (rs[3][1] - rs[3][0]) * 3 + 8

@@ -156,10 +156,22 @@ static void fill_bases(MsmBases& b, const uint8_t* src, size_t count, size_t at,
   b.extend(st);
 }
 
-// [lo, hi) of slice `part` when n items are cut into nparts contiguous ranges
+// [lo, hi) of slice `part` when n items are cut into nparts contiguous ranges.  With
+// ZKP_SPLIT_BALANCE=1 (a split proof with the distributed quotient) the parts that extend a
+// quotient vector (parts 0..min(3, nparts)-1: rank v % G extends vector v) get weight 3 and the
+// others 8, so their coset extension (~6 ms at S24) is offset by fewer points; lo = n W_<k / W
+// in integers (zkp_amd.dist.split_range and oracle.groth16.split_range compute the same).
 static void split_range(size_t n, int part, int nparts, size_t& lo, size_t& hi) {
-  lo = n * (size_t)part / (size_t)nparts;
-  hi = n * (size_t)(part + 1) / (size_t)nparts;
+  const char* e = std::getenv("ZKP_SPLIT_BALANCE");
+  if (!(e && std::atoi(e) == 1) || nparts <= 3) {
+    lo = n * (size_t)part / (size_t)nparts;
+    hi = n * (size_t)(part + 1) / (size_t)nparts;
+    return;
+  }
+  auto cum = [&](int k) { return (size_t)3 * std::min(k, 3) + (size_t)8 * std::max(k - 3, 0); };
+  const size_t total = cum(nparts);
+  lo = n * cum(part) / total;
+  hi = n * cum(part + 1) / total;
 }
 
 // A long-lived host thread that runs one job at a time (the per-proof G1 / G2 enqueue jobs of a
