@@ -170,7 +170,7 @@ def run_split(args, rank, world, local):
     import torch
     if args.quotient == "dist":
         # the quotient-vector owners (parts 0..2) take fewer points (prover.hip split_range; every
-        # rank and the slice exchange read the same setting): S24 over 8 slices 13.3 -> 10.3 ms
+        # rank and the slice exchange read the same setting): S24 over 8 slices 13.3 -> 9.7 ms
         os.environ.setdefault("ZKP_SPLIT_BALANCE", "1")
     scale = args.scale
     circ = synth.Circuit(int(S24["n_vars"] * scale), int(S24["n_constraints"] * scale), S24["n_public"], CIRCUIT_SEED)

@@ -91,10 +91,11 @@ def prove(z: ZKey, w, r: int, s: int):
 def split_range(n: int, part: int, nparts: int, balance: bool = False):
     """[lo, hi) of slice `part` of n items in nparts contiguous ranges (as prover.hip split_range);
     balance (ZKP_SPLIT_BALANCE=1 there): for nparts > 3, parts 0..2 (the quotient-vector owners)
-    weigh 3 and the others 8."""
+    weigh max(1, 11 - nparts) and the others 11."""
     if not balance or nparts <= 3:
         return n * part // nparts, n * (part + 1) // nparts
-    cum = lambda k: 3 * min(k, 3) + 8 * max(k - 3, 0)  # noqa: E731
+    wq = max(1, 11 - nparts)  # see prover.hip split_range
+    cum = lambda k: wq * min(k, 3) + 11 * max(k - 3, 0)  # noqa: E731
     return n * cum(part) // cum(nparts), n * cum(part + 1) // cum(nparts)
 
 

@@ -179,12 +179,13 @@ def test_split_blinding_agreed_gloo_world2():
 def test_split_ranges_agree(balance):
     # zkp_amd.dist.split_range (the exchange, the emulation) and the oracle's (partial sums) give
     # the same contiguous tiling of [0, n) -- the C++ split_range is checked against them through
-    # the GPU split tests; balanced: parts 0..2 weigh 3, the others 8 (nparts > 3)
+    # the GPU split tests; balanced: parts 0..2 weigh max(1, 11 - G), the others 11 (nparts > 3)
     from zkp_amd.dist import split_range
     for n in (1, 7, 100, 1 << 21, 6_400_562):
         for nparts in range(1, 10):
             rs = [split_range(n, k, nparts, balance) for k in range(nparts)]
             assert rs == [groth16.split_range(n, k, nparts, balance) for k in range(nparts)]
             assert rs[0][0] == 0 and rs[-1][1] == n and all(rs[k][1] == rs[k + 1][0] for k in range(nparts - 1))
-            if balance and nparts > 3 and n >= 1 << 21:
-                assert (rs[0][1] - rs[0][0]) * 8 < (rs[3][1] - rs[3][0]) * 3 + 8
+            if balance and nparts > 3 and n >= 1 << 21:  # weights max(1, 11 - G) : 11
+                wq = max(1, 11 - nparts)
+                assert abs((rs[0][1] - rs[0][0]) * 11 - (rs[3][1] - rs[3][0]) * wq) <= 11 * 11

@@ -157,10 +157,12 @@ static void fill_bases(MsmBases& b, const uint8_t* src, size_t count, size_t at,
 }
 
 // [lo, hi) of slice `part` when n items are cut into nparts contiguous ranges.  With
-// ZKP_SPLIT_BALANCE=1 (a split proof with the distributed quotient) the parts that extend a
-// quotient vector (parts 0..min(3, nparts)-1: rank v % G extends vector v) get weight 3 and the
-// others 8, so their coset extension (~6 ms at S24) is offset by fewer points; lo = n W_<k / W
-// in integers (zkp_amd.dist.split_range and oracle.groth16.split_range compute the same).
+// ZKP_SPLIT_BALANCE=1 (a split proof with the distributed quotient) and G = nparts > 3, the parts
+// that extend a quotient vector (0..2: rank v % G extends vector v) get weight max(1, 11 - G) and
+// the others 11: with one coset extension costing r = 1/8 of the proof's MSM work M (S24: ~6.6 of
+// ~53 ms), Q + M s_q = M s_o and 3 s_q + (G - 3) s_o = 1 give s_q = (11 - G) / (8 G),
+// s_o = 11 / (8 G).  lo = n W_<k / W in integers (zkp_amd.dist.split_range and
+// oracle.groth16.split_range compute the same).
 static void split_range(size_t n, int part, int nparts, size_t& lo, size_t& hi) {
   const char* e = std::getenv("ZKP_SPLIT_BALANCE");
   if (!(e && std::atoi(e) == 1) || nparts <= 3) {
@@ -168,7 +170,8 @@ static void split_range(size_t n, int part, int nparts, size_t& lo, size_t& hi) 
     hi = n * (size_t)(part + 1) / (size_t)nparts;
     return;
   }
-  auto cum = [&](int k) { return (size_t)3 * std::min(k, 3) + (size_t)8 * std::max(k - 3, 0); };
+  const size_t wq = (size_t)std::max(1, 11 - nparts);
+  auto cum = [&](int k) { return wq * (size_t)std::min(k, 3) + (size_t)11 * (size_t)std::max(k - 3, 0); };
   const size_t total = cum(nparts);
   lo = n * cum(part) / total;
   hi = n * cum(part + 1) / total;

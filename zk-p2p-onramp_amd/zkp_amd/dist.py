@@ -27,13 +27,14 @@ from . import PARTIAL_BYTES, Prover, proof_combine_raw
 def split_range(n: int, part: int, nparts: int, balance=None):
     """[lo, hi) of slice `part` of n items cut into nparts contiguous ranges (as the C++
     split_range in prover.hip).  balance (default: ZKP_SPLIT_BALANCE=1 in the environment, which
-    the C++ side reads too): for nparts > 3 the parts that extend a quotient vector (0..2) weigh 3,
-    the others 8."""
+    the C++ side reads too): for nparts > 3 the parts that extend a quotient vector (0..2) weigh
+    max(1, 11 - nparts), the others 11."""
     if balance is None:
         balance = os.environ.get("ZKP_SPLIT_BALANCE") == "1"
     if not balance or nparts <= 3:
         return n * part // nparts, n * (part + 1) // nparts
-    cum = lambda k: 3 * min(k, 3) + 8 * max(k - 3, 0)  # noqa: E731
+    wq = max(1, 11 - nparts)  # see prover.hip split_range
+    cum = lambda k: wq * min(k, 3) + 11 * max(k - 3, 0)  # noqa: E731
     return n * cum(part) // cum(nparts), n * cum(part + 1) // cum(nparts)
 
 
