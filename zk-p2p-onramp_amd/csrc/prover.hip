@@ -816,8 +816,9 @@ Prover::~Prover() = default;
 // snarkjs groth16_prove's blinding, in two phases: everything but piH
 // (assemble_pre: runs while the H MSM is still on the device) and C + piH + the encoding.
 struct Blinded {
-  Jac<HFq> A, Cpart;  // Cpart = piC' + s A + r B1 - (r s) delta1
-  Jac<HFq2> B;
+  Jac<HFq> Cpart;  // piC' + s A + r B1 - (r s) delta1
+  Affine<HFq> a;   // A and B are final here: converted to affine before piH exists
+  Affine<HFq2> b;
 };
 static Blinded assemble_pre(const ZkeyHeader& h, const DevicePipeline::MsmOut& m, const uint8_t* r32,
                             const uint8_t* s32) {
@@ -827,23 +828,25 @@ static Blinded assemble_pre(const ZkeyHeader& h, const DevicePipeline::MsmOut& m
   const Jac<HFq2> beta2 = host::jac_from_aff(h.beta2), delta2 = host::jac_from_aff(h.delta2);
   Blinded o;
   // A = piA' + alpha1 + r delta1
-  o.A = host::jac_add(host::jac_add(m.a, alpha1), host::jac_mul(delta1, r));
+  const Jac<HFq> A = host::jac_add(host::jac_add(m.a, alpha1), host::jac_mul(delta1, r));
   // B = piB' + beta2 + s delta2 ; B1 = piB1' + beta1 + s delta1
-  o.B = host::jac_add(host::jac_add(m.b2, beta2), host::jac_mul(delta2, s));
+  const Jac<HFq2> B = host::jac_add(host::jac_add(m.b2, beta2), host::jac_mul(delta2, s));
   Jac<HFq> B1 = host::jac_add(host::jac_add(m.b1, beta1), host::jac_mul(delta1, s));
   // C = piC' + piH + s A + r B1 - (r s) delta1
   HFr rs = HFr::from_std(r) * HFr::from_std(s);
   U256 nrs = rs.neg().to_std();
   Jac<HFq> C = m.c;
-  C = host::jac_add(C, host::jac_mul(o.A, s));
+  C = host::jac_add(C, host::jac_mul(A, s));
   C = host::jac_add(C, host::jac_mul(B1, r));
   o.Cpart = host::jac_add(C, host::jac_mul(delta1, nrs));
+  o.a = host::jac_to_aff(A);
+  o.b = host::jac_to_aff(B);
   return o;
 }
 static void assemble_post(const ZkeyHeader& h, const Blinded& bl, const Jac<HFq>& piH, const WtnsView& w,
                           zkp_proof* out) {
-  auto a = host::jac_to_aff(bl.A);
-  auto b = host::jac_to_aff(bl.B);
+  const Affine<HFq>& a = bl.a;
+  const Affine<HFq2>& b = bl.b;
   auto c = host::jac_to_aff(host::jac_add(bl.Cpart, piH));
   put_fq(a.x, out->pi_a[0]);
   put_fq(a.y, out->pi_a[1]);
