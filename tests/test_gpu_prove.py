@@ -185,3 +185,23 @@ def test_concurrent_prove_on_one_handle(golden_dir):
     for t in th:
         t.join()
     assert not errs and got == want
+
+
+@pytest.mark.parametrize("circuit", ["small", "venmo_mini"])
+def test_batch_inflight_shared_tables(golden_dir, monkeypatch, circuit):
+    """ZKP_INFLIGHT=3: three pipelines on device 0 share one copy of the base tables; a batch
+    over them (several proofs in flight at once) and round-robin single proofs on each
+    pipeline all reproduce the golden proof bit-exactly."""
+    monkeypatch.setenv("ZKP_INFLIGHT", "3")
+    zk, wt = _files(golden_dir, circuit)
+    man = json.load(open(os.path.join(golden_dir, "manifest.json")))["circuits"][circuit]
+    r, s = int(man["r"]), int(man["s"])
+    p = zkp_amd.Prover(zk)
+    want = open(os.path.join(golden_dir, "proof_%s.json" % circuit)).read()
+    n = 9
+    res, st = p.prove_batch_status_raw([wt] * n, [r] * n, [s] * n)
+    assert st == [0] * n
+    for (a, b, c), _ in res:
+        assert groth16.js_stringify(zkp_amd.proof_object(a, b, c)) == want
+    for _ in range(3):  # zkp_prove round-robins over the three pipelines
+        assert groth16.js_stringify(p.prove(wt, r=r, s=s)["proof"]) == want

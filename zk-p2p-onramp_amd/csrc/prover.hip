@@ -229,7 +229,11 @@ class DevicePipeline {
  public:
   // part / nparts: this pipeline holds only slice `part` of every point section (the
   // point-range split of one proof over several GPUs); 0 / 1 = all
-  DevicePipeline(int dev, const ZkeyParsed& z, int part = 0, int nparts = 1) : dev_(dev), hdr_(z.hdr) {
+  // share: another pipeline of the same device and slice whose base tables (the ~38 GB of
+  // precomputed points) this one uses instead of building its own (ZKP_INFLIGHT > 1: several
+  // proofs in flight per device, each with its own streams, plans, engines and buffers)
+  DevicePipeline(int dev, const ZkeyParsed& z, int part = 0, int nparts = 1, const DevicePipeline* share = nullptr)
+      : dev_(dev), hdr_(z.hdr) {
     HIPX(hipSetDevice(dev_));
     // s0 carries the critical path (quotient -> H plan -> H MSM): highest priority, so the
     // A/B1/C (s2) and B2 (s1) MSMs fill the CUs it leaves idle instead of delaying it
@@ -271,21 +275,28 @@ class DevicePipeline {
     choose_msm_params(nv, nd, pw, ph);
     // base tables: A, B1, C, B2 indexed by witness signal (C's first nPublic+1 bases are
     // infinity, so one witness plan serves all four), H by domain index
-    ta_ = std::make_unique<MsmBases>(Curve::G1, nv, pw.c, pw.depth);
-    tb1_ = std::make_unique<MsmBases>(Curve::G1, nv, pw.c, pw.depth);
-    tc_ = std::make_unique<MsmBases>(Curve::G1, nv, pw.c, pw.depth);
-    tb2_ = std::make_unique<MsmBases>(Curve::G2, nv, pw.c, pw.depth);
-    th_ = std::make_unique<MsmBases>(Curve::G1, nd, ph.c, ph.depth);
-    fill_bases(*ta_, z.bf.sec[5].ptr + wlo_ * 64, nv, 0, s0_);
-    fill_bases(*tb1_, z.bf.sec[6].ptr + wlo_ * 64, nv, 0, s0_);
-    fill_bases(*tb2_, z.bf.sec[7].ptr + wlo_ * 128, nv, 0, s0_);
-    {
-      const size_t cfirst = std::max(wlo_, c0);  // first witness index of the slice with a C base
-      const size_t lead = std::min(cfirst, whi_) - wlo_;
-      const size_t cnt = whi_ > cfirst ? whi_ - cfirst : 0;
-      fill_bases(*tc_, cnt ? z.bf.sec[8].ptr + (cfirst - c0) * 64 : nullptr, cnt, lead, s0_);
+    if (share) {
+      if (share->dev_ != dev_ || share->wlo_ != wlo_ || share->whi_ != whi_ || share->hlo_ != hlo_ ||
+          share->hhi_ != hhi_)
+        throw ZkpError(ZKP_ERR_INTERNAL, "shared base tables of another device or slice");
+      ta_ = share->ta_, tb1_ = share->tb1_, tc_ = share->tc_, tb2_ = share->tb2_, th_ = share->th_;
+    } else {
+      ta_ = std::make_shared<MsmBases>(Curve::G1, nv, pw.c, pw.depth);
+      tb1_ = std::make_shared<MsmBases>(Curve::G1, nv, pw.c, pw.depth);
+      tc_ = std::make_shared<MsmBases>(Curve::G1, nv, pw.c, pw.depth);
+      tb2_ = std::make_shared<MsmBases>(Curve::G2, nv, pw.c, pw.depth);
+      th_ = std::make_shared<MsmBases>(Curve::G1, nd, ph.c, ph.depth);
+      fill_bases(*ta_, z.bf.sec[5].ptr + wlo_ * 64, nv, 0, s0_);
+      fill_bases(*tb1_, z.bf.sec[6].ptr + wlo_ * 64, nv, 0, s0_);
+      fill_bases(*tb2_, z.bf.sec[7].ptr + wlo_ * 128, nv, 0, s0_);
+      {
+        const size_t cfirst = std::max(wlo_, c0);  // first witness index of the slice with a C base
+        const size_t lead = std::min(cfirst, whi_) - wlo_;
+        const size_t cnt = whi_ > cfirst ? whi_ - cfirst : 0;
+        fill_bases(*tc_, cnt ? z.bf.sec[8].ptr + (cfirst - c0) * 64 : nullptr, cnt, lead, s0_);
+      }
+      fill_bases(*th_, z.bf.sec[9].ptr + hlo_ * 64, nd, 0, s0_);
     }
-    fill_bases(*th_, z.bf.sec[9].ptr + hlo_ * 64, nd, 0, s0_);
     for (int m = 0; m < 2; ++m) {
       const Csr& c = z.csr[m];
       HIPX(hipMalloc(&rowptr_[m], c.rowptr.size() * 4));
@@ -744,7 +755,7 @@ class DevicePipeline {
   hipStream_t s4_ = nullptr;  // H plan on the reserved CUs (ZKP_RESERVE_CUS > 0), else s0
   hipEvent_t ev_[16];
   JobThread jt_g1_, jt_g2_;  // host threads feeding s2 (witness plan, G1 MSMs) and s1 (G2 MSM)
-  std::unique_ptr<MsmBases> ta_, tb1_, tc_, tb2_, th_;
+  std::shared_ptr<MsmBases> ta_, tb1_, tc_, tb2_, th_;  // shared by the pipelines of one device
   uint32_t* rowptr_[2] = {nullptr, nullptr};
   uint32_t* col_[2] = {nullptr, nullptr};
   uint32_t* val_[2] = {nullptr, nullptr};
@@ -790,9 +801,14 @@ Prover::Prover(const uint8_t* zkey, size_t len, const std::vector<int>& devices,
   HIPX(hipGetDeviceCount(&ndev));
   if (ndev <= 0) throw ZkpError(ZKP_ERR_DEVICE, "no HIP device available");
   std::vector<int> devs = devices.empty() ? std::vector<int>{0} : devices;
+  // ZKP_INFLIGHT = k > 1: k pipelines per device sharing its base tables, so zkp_prove_batch
+  // (one worker per pipeline) and concurrent zkp_prove callers keep k proofs in flight per GPU
+  const int inflight = std::max(1, std::min(4, env_int("ZKP_INFLIGHT", 1)));
   for (int d : devs) {
     if (d < 0 || d >= ndev) throw ZkpError(ZKP_ERR_INVALID_ARG, "device ordinal out of range");
     devs_.push_back(std::make_unique<DevicePipeline>(d, z, part, nparts));
+    const DevicePipeline* first = devs_.back().get();
+    for (int k = 1; k < inflight; ++k) devs_.push_back(std::make_unique<DevicePipeline>(d, z, part, nparts, first));
   }
   // test hook: pipeline ZKP_TEST_FAIL_PIPELINE reports a device failure after
   // ZKP_TEST_FAIL_AFTER proofs (exercises the batch re-queue; never set in production)
