@@ -3,7 +3,7 @@
 set -e
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out/prof
-B="python3 bench.py --steps 4 --warmup 1 --cpu-baseline none --no-kernels"
+B="python3 bench.py --steps 4 --warmup 1 --cpu-baseline none --no-kernels --batch 0"  # headline loop only: the batch line runs two proofs in flight per GPU, whose contended launches would skew the per-kernel averages
 W=/tmp/zkp_prof
 rm -rf $W && mkdir -p $W
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $W/conc -o run -- $B > gpurun_out/prof/conc.log 2>&1
