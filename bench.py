@@ -9,11 +9,21 @@ real 3.5 GB zkey / witness are absent.  Insecure known-tau set
 
 A "step" = one complete proof (buildABC, 3 coset NTTs, joinABC, 4 G1 + 1 G2 MSMs,
 blinding) of one distinct synthetic witness already resident in HBM (staged).
-Multi-GPU (torchrun --nproc-per-node N): every rank proves its own witnesses on its
-own GPU (replicas, no collectives: SURVEY.md §8e E1(1)); value = all proofs / max
-rank time.  Extra fields: latency, per-stage ms, config-2 kernels (G1 MSM 2^20
-Mpts/s, Fr NTT 2^20), roofline of the bucket-accumulate kernel (HIP events), and
-the C++ CPU restatement (oracle/cpu) timed on this host as cpu_baseline.
+
+Multi-GPU = replicas, no collectives (SURVEY.md §8e E1(1), configs[3]); value = all
+proofs / wall time (max over ranks), n_gpus = devices actually used:
+  * `torchrun --nproc-per-node N bench.py --gpus N`: one process per GPU (LOCAL_RANK),
+    each with its own resident key; gloo carries only the barrier and the max.
+  * `python bench.py --gpus N` (no torchrun): ONE process, one resident prover over
+    devices [0..N-1] (zkp_prover_load with N devices), one host thread per device running
+    staged proofs concurrently.  Fewer than N visible devices -> exit status 2 with a
+    message, never a silent 1-GPU line.  `--rehearsal` maps the N logical devices onto
+    device 0 (pipelines sharing one copy of the base tables) and marks the line
+    "rehearsal": true -- a check of the multi-device code path, not a scaling number.
+Every timed proof and every batch proof is compared with a separately computed proof of
+the same witness at the same r, s.  Extra fields: latency, per-stage ms, config-1 kernels
+(G1 MSM 2^20 Mpts/s, Fr NTT 2^20 / 2^23), roofline of the bucket-accumulate kernel (HIP
+events), and the C++ CPU restatement (oracle/cpu) timed on this host as cpu_baseline.
 """
 import argparse
 import json
@@ -83,6 +93,15 @@ def gen_witnesses(circ, seeds):
     for t in ths:
         t.join()
     return out
+
+
+def visible_devices():
+    """GPUs this process can use (counting does not initialise the GPU on this image)."""
+    try:
+        import torch
+        return torch.cuda.device_count()
+    except Exception:
+        return 0
 
 
 def host_cpu_info():
@@ -269,22 +288,25 @@ def run_split(args, rank, world, local):
     print(json.dumps(out), flush=True)
 
 
-def batch_pcie_inclusive(args, circ, prover, wit, rank, world, dist, sync, r_fix, s_fix):
+def batch_pcie_inclusive(args, circ, prover, wit, refs, rank, world, ndev, dist, sync, r_fix, s_fix):
     """configs[3] with the witness upload included: args.batch proofs per rank through
-    zkp_prove_batch from HOST memory (args.batch_distinct distinct witnesses cycled; every
-    proof copies its witness over PCIe), two workers per device so the next witness's H2D
-    overlaps the current proof.  One warm-up proof per worker first.  Whole-job proofs/s
-    (max over ranks), for comparison with the staged headline."""
+    zkp_prove_batch from HOST memory over all of this process's devices (args.batch_distinct
+    distinct witnesses cycled; every proof copies its witness over PCIe), two workers per
+    pipeline so the next witness's H2D overlaps the current proof.  One warm-up call first.
+    Every batch proof is compared with a separately computed proof of the same witness (the
+    staged reference proofs, or one zkp_prove per extra witness before the timed region).
+    Whole-job proofs/s (max over ranks), for comparison with the staged headline."""
     k = max(1, args.batch_distinct)
     extra = gen_witnesses(circ, [500000 + 1000 * rank + i for i in range(max(0, k - len(wit)))])
     host = (list(wit) + extra)[:k]
-    order = [host[i % k] for i in range(args.batch)]
+    ref = list(refs[:len(host)]) + [prover.prove_raw(w, r_fix, s_fix) for w in host[len(refs):]]
+    order = [i % k for i in range(args.batch)]
     prover.prove_batch_raw(host[:2], [r_fix] * 2, [s_fix] * 2)
     if dist:
         dist.barrier()
     sync()
     t0 = time.perf_counter()
-    res = prover.prove_batch_raw(order, [r_fix] * len(order), [s_fix] * len(order))
+    res = prover.prove_batch_raw([host[i] for i in order], [r_fix] * len(order), [s_fix] * len(order))
     sync()
     el = time.perf_counter() - t0
     if dist:
@@ -292,13 +314,15 @@ def batch_pcie_inclusive(args, circ, prover, wit, rank, world, dist, sync, r_fix
         t = torch.tensor([el], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
-    ok = len(res) == len(order) and all(r is not None for r in res)
-    return {"proofs_per_rank": len(order), "distinct_host_witnesses": k, "n_gpus": world,
+    bad = [j for j in range(len(order)) if j >= len(res) or res[j] != ref[order[j]]]
+    return {"proofs_per_rank": len(order), "distinct_host_witnesses": k, "n_gpus": world * ndev,
             "proofs_per_s": round(len(order) * world / el, 3), "ms_per_proof": round(el / len(order) * 1e3, 3),
-            "all_proofs_ok": ok, "pipelines_per_device": int(os.environ.get("ZKP_INFLIGHT", "1")),
+            "all_proofs_ok": len(res) == len(order) and not bad, "mismatched_proofs": bad[:8],
+            "check": "every batch proof == a separately computed proof of the same witness at the same r, s",
+            "pipelines_per_device": int(os.environ.get("ZKP_INFLIGHT", "1")),
             "workers_per_pipeline": 2,
-            "note": "zkp_prove_batch from pageable host memory: the 205 MB witness H2D of proof i+1 runs on an "
-                    "upload-slot stream while proof i computes"}
+            "note": "zkp_prove_batch from pageable host memory over %d device(s): the 205 MB witness H2D of "
+                    "proof i+1 runs on an upload-slot stream while proof i computes" % ndev}
 
 
 def cpu_baseline(args, zk, wit0, gpu_proof, r_fix, s_fix, msm_case):
@@ -359,6 +383,9 @@ def main():
     ap.add_argument("--mode", choices=["replicas", "split"], default="replicas",
                     help="replicas: independent proofs per GPU (headline); split: configs[4], one proof over GPUs")
     ap.add_argument("--parts", type=int, default=2, help="split mode in one process: slices on one GPU")
+    ap.add_argument("--rehearsal", action="store_true",
+                    help="--gpus N without torchrun on fewer GPUs: N logical devices on one GPU (code-path check; "
+                         "the line says \"rehearsal\": true and is not a scaling number)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -375,8 +402,29 @@ def main():
             tdist.init_process_group("nccl")  # RCCL: the partial-sum all-gather runs over xGMI
         return run_split(args, rank, world, local)
     if world > 1:
+        if args.gpus not in (1, world):
+            log("bench.py: --gpus %d but torchrun started %d ranks (one GPU per rank)" % (args.gpus, world))
+            sys.exit(2)
         import torch.distributed as dist  # noqa: F811
         dist.init_process_group("gloo")  # measurement plumbing only (barrier / max); the path has no collective
+        devices, rehearsal = [local], False
+    else:
+        # one process driving N devices (one host process, a resident key per GPU)
+        if args.gpus < 1:
+            log("bench.py: --gpus must be >= 1")
+            sys.exit(2)
+        rehearsal = args.rehearsal and args.gpus > 1
+        if rehearsal:
+            devices = [local] * args.gpus
+        else:
+            visible = visible_devices()
+            if visible < args.gpus:
+                log("bench.py: --gpus %d requested but only %d GPU(s) visible; refusing to report a %d-GPU "
+                    "number from fewer devices (use --rehearsal to map %d logical devices onto device %d)"
+                    % (args.gpus, visible, args.gpus, args.gpus, local))
+                sys.exit(2)
+            devices = list(range(args.gpus)) if args.gpus > 1 else [local]
+    ndev = len(devices)
 
     t_setup = time.time()
     if args.scale == 1.0:
@@ -391,38 +439,65 @@ def main():
     log("[rank %d] circuit + %d witnesses: %.1fs" % (rank, nw, time.time() - t_setup))
     t0 = time.time()
     # host threads for the synthetic key's QAP evaluation: share the host between the ranks
-    zk = circ.zkey(SETUP_SEED, device=local, threads=max(1, (os.cpu_count() or 8) // max(1, world)))
+    zk = circ.zkey(SETUP_SEED, device=devices[0], threads=max(1, (os.cpu_count() or 8) // max(1, world)))
     log("[rank %d] synthetic zkey (%.2f GB): %.1fs" % (rank, zk.len / 1e9, time.time() - t0))
     t0 = time.time()
     # two pipelines per device sharing the base tables: the batch line keeps two proofs in
     # flight per GPU (+2.4% measured, profiles/inflight_r02.txt); the staged headline runs on
-    # pipeline 0 alone either way
+    # each device's first pipeline
     os.environ.setdefault("ZKP_INFLIGHT", "2")
-    prover = zkp_amd.Prover(zk, devices=[local])
-    for i, w in enumerate(wit):
-        prover.stage(w, slot=i)
-    log("[rank %d] zkey resident in HBM + witnesses staged: %.1fs" % (rank, time.time() - t0))
+    prover = zkp_amd.Prover(zk, devices=devices)
+    for d in range(ndev):
+        for i, w in enumerate(wit):
+            prover.stage(w, slot=i, dev_index=d)
+    log("[rank %d] zkey resident in HBM of %d device(s) %s + witnesses staged: %.1fs"
+        % (rank, ndev, devices, time.time() - t0))
 
     R_FIX, S_FIX = 0x1234567, 0x7654321
-    for i in range(args.warmup):
-        prover.prove_staged_raw(i % nw, R_FIX, S_FIX)
+
+    def on_devices(fn):
+        """fn(d) for every device index, concurrently (one host thread per device)."""
+        if ndev == 1:
+            fn(0)
+            return
+        errs = []
+
+        def run(d):
+            try:
+                fn(d)
+            except BaseException as e:  # re-raised below
+                errs.append(e)
+        ths = [threading.Thread(target=run, args=(d,)) for d in range(ndev)]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+        if errs:
+            raise errs[0]
+
+    on_devices(lambda d: [prover.prove_staged_raw(i % nw, R_FIX, S_FIX, dev_index=d) for i in range(args.warmup)])
+    # reference proofs of the staged witnesses (device 0), computed before the timed region
+    refs = [prover.prove_staged_raw(i, R_FIX, S_FIX, dev_index=0) for i in range(nw)]
     prover.instrument(True)
 
     def sync():
         try:
             import torch
             if torch.cuda.is_available():
-                torch.cuda.synchronize(local)
+                for d in sorted(set(devices)):
+                    torch.cuda.synchronize(d)
         except Exception:
             pass
 
     if dist:
         dist.barrier()
     sync()
+    per_dev = [None] * ndev
+
+    def timed(d):
+        per_dev[d] = [prover.prove_staged_raw(i % nw, R_FIX, S_FIX, dev_index=d) for i in range(args.steps)]
     t_start = time.perf_counter()
-    results = []
-    for i in range(args.steps):
-        results.append(prover.prove_staged_raw(i % nw, R_FIX, S_FIX))
+    on_devices(timed)
     sync()
     elapsed = time.perf_counter() - t_start
     if dist:
@@ -431,6 +506,8 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
         dist.barrier()
+    results = per_dev[0]
+    mismatch = [(d, i) for d in range(ndev) for i in range(args.steps) if per_dev[d][i] != refs[i % nw]]
     kstats = prover.kernel_stats()
     msm_cfg = prover.msm_config()
     stage_ms = prover.timings()
@@ -442,12 +519,12 @@ def main():
 
     batch = None
     if args.batch > 0:
-        batch = batch_pcie_inclusive(args, circ, prover, wit, rank, world, dist, sync, R_FIX, S_FIX)
+        batch = batch_pcie_inclusive(args, circ, prover, wit, refs, rank, world, ndev, dist, sync, R_FIX, S_FIX)
 
     if rank != 0:
         return
 
-    n_total = args.steps * world
+    n_total = args.steps * world * ndev
     value = n_total / elapsed
     ms_per_step = elapsed / args.steps * 1e3
     g1 = kstats["g1"]
@@ -484,7 +561,7 @@ def main():
         "metric": "Groth16 proofs/sec (node) + 1-proof latency, Venmo circuit; G1 MSM Mpts/s",
         "value": round(value, 4),
         "unit": "proofs/s",
-        "n_gpus": world,
+        "n_gpus": world * ndev,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 3),
@@ -499,17 +576,28 @@ def main():
                    "n_vars": circ.n_vars, "n_constraints": circ.n_constraints, "n_public": circ.n_public,
                    "domain": circ.domain_size, "distinct_witnesses_per_rank": nw,
                    "witness_bool_pct": args.bool_pct,
-                   "parallelism": "replicas%d" % world, "msm": msm_cfg},
+                   "parallelism": "replicas%d" % (world * ndev),
+                   "launch": "torchrun, one process per GPU" if world > 1 else
+                             "one process, one resident prover over devices %s, one host thread per device" % devices,
+                   "msm": msm_cfg},
+        "all_proofs_ok": not mismatch,
+        "proof_check": "every timed proof == the reference proof of the same staged witness (device 0, same r, s)",
         "stage_ms_last_proof": {k: round(v, 3) for k, v in stage_ms.items()},
         "batch_pcie_inclusive": batch,
         "roofline": roofline,
     }
 
+    if rehearsal:
+        out["rehearsal"] = True
+        out["rehearsal_note"] = ("%d logical devices mapped onto GPU %d (pipelines sharing one copy of the base "
+                                 "tables): exercises the multi-device path; not a scaling measurement" % (ndev, local))
+    if mismatch:
+        out["mismatched_proofs"] = mismatch[:8]
     msm_case = None
     if batch:
         batch["vs_staged_headline"] = round(batch["proofs_per_s"] / value, 4)
     if not args.no_kernels:
-        kb, kst, msm_case = kernel_benches(local)
+        kb, kst, msm_case = kernel_benches(devices[0])
         out["kernels_config1"] = kb
         if peak and kst["ms_accumulate"] > 0:
             # the same kernel alone on the GPU (configs[1] G1 MSM 2^20, uniform scalars): the in-proof

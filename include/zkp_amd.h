@@ -42,9 +42,12 @@ typedef enum zkp_status {
 
 /* Opaque prover handle: parsed + validated zkey whose point sections are resident in
  * HBM of every device in the list (uploaded once at load).  Immutable after load;
- * concurrent zkp_prove calls on one handle are safe: each takes one of two witness
- * upload slots of its device (its H2D overlaps the proof in flight), the proofs
- * themselves run one at a time per device (one proof saturates an MI355X). */
+ * concurrent zkp_prove calls on one handle are safe.  Each device holds k proving
+ * pipelines (environment ZKP_INFLIGHT = k, 1..4, default 1) that share one copy of its
+ * base tables: up to k proofs run concurrently per device, each pipeline one at a time,
+ * and each pipeline has two witness upload slots (a witness H2D overlaps the proof in
+ * flight).  zkp_prove round-robins over the healthy pipelines; zkp_prove_batch runs two
+ * workers per pipeline. */
 typedef struct zkp_prover zkp_prover;
 
 /* One Groth16 proof: affine coordinates, standard-form LE (the pi_a/pi_b/pi_c of
@@ -198,8 +201,10 @@ zkp_status zkp_ntt_fr(int device, uint8_t* data, size_t n, int mode);
 zkp_status zkp_quotient(zkp_prover* p, const uint8_t* wtns, size_t len, uint8_t* out);
 
 /* ---- benchmarking / serving helpers ----
- * Keep a witness resident in HBM (device index into the prover's device list, any
- * slot number); zkp_prove_staged then runs the proof without the PCIe copy. */
+ * Keep a witness resident in HBM (dev_index: index into the `devices` list the prover was
+ * loaded with, 0..ndev-1, whatever ZKP_INFLIGHT is; the witness goes to that device's first
+ * pipeline; any slot number); zkp_prove_staged then runs the proof without the PCIe copy on
+ * the same pipeline.  Calls for different dev_index values run concurrently. */
 zkp_status zkp_witness_stage(zkp_prover* p, int dev_index, int slot, const uint8_t* wtns, size_t len);
 zkp_status zkp_prove_staged(zkp_prover* p, int dev_index, int slot, const uint8_t* r32, const uint8_t* s32,
                             zkp_proof* out);

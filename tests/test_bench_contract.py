@@ -55,3 +55,21 @@ def test_cpu_baseline(name):
     assert c["kind"] in ("port", "reference")
     assert c["cores"] >= 1 and c["value"] > 0 and c["sample"]
     assert c.get("bit_exact_vs_gpu") is True
+
+
+def test_gpus_more_than_visible_fails_loudly():
+    """`bench.py --gpus N` without torchrun drives N devices from one process; with fewer
+    visible GPUs (none here, one on the test box) it must exit non-zero with a message instead
+    of printing a line measured on fewer devices."""
+    import os
+    import subprocess
+    import sys
+    root = PROFILES.parent
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    p = subprocess.run([sys.executable, str(root / "bench.py"), "--gpus", "64", "--cpu-baseline", "none"],
+                       cwd=str(root), env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 2, (p.returncode, p.stderr[-2000:])
+    assert "--gpus 64 requested" in p.stderr and "--rehearsal" in p.stderr
+    assert p.stdout.strip() == ""

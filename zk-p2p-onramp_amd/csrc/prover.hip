@@ -438,6 +438,7 @@ class DevicePipeline {
   void set_fault_injection(int after) { fail_after_ = after; }
   bool healthy() const { return healthy_.load(); }
   void mark_failed() { healthy_.store(false); }
+  int device() const { return dev_; }
 
   // quotient (rows A4..A8) from a device-resident witness; result scalars in pscal_
   void enqueue_quotient(const uint32_t* d_wit) {
@@ -803,12 +804,41 @@ Prover::Prover(const uint8_t* zkey, size_t len, const std::vector<int>& devices,
   std::vector<int> devs = devices.empty() ? std::vector<int>{0} : devices;
   // ZKP_INFLIGHT = k > 1: k pipelines per device sharing its base tables, so zkp_prove_batch
   // (one worker per pipeline) and concurrent zkp_prove callers keep k proofs in flight per GPU
-  const int inflight = std::max(1, std::min(4, env_int("ZKP_INFLIGHT", 1)));
-  for (int d : devs) {
+  // devs_ holds inflight_ consecutive pipelines per entry of `devices`; the staged entry points'
+  // dev_index names an entry of `devices` (its first pipeline).  An ordinal listed twice (a
+  // multi-device rehearsal on one GPU) shares the base tables of its first listing.
+  inflight_ = std::max(1, std::min(4, env_int("ZKP_INFLIGHT", 1)));
+  for (int d : devs)
     if (d < 0 || d >= ndev) throw ZkpError(ZKP_ERR_INVALID_ARG, "device ordinal out of range");
-    devs_.push_back(std::make_unique<DevicePipeline>(d, z, part, nparts));
-    const DevicePipeline* first = devs_.back().get();
-    for (int k = 1; k < inflight; ++k) devs_.push_back(std::make_unique<DevicePipeline>(d, z, part, nparts, first));
+  ndevices_ = (int)devs.size();
+  devs_.resize((size_t)ndevices_ * inflight_);
+  // the first listing of every ordinal builds its base tables (upload + row derivation, ~2 s
+  // for the Venmo key): one host thread per GPU, so an 8-GPU load takes as long as one
+  std::vector<int> owner(ndevices_, -1);  // entry whose tables entry e shares (-1: builds its own)
+  for (int e = 0; e < ndevices_; ++e)
+    for (int f = 0; f < e && owner[e] < 0; ++f)
+      if (devs[f] == devs[e] && owner[f] < 0) owner[e] = f;
+  {
+    std::vector<std::exception_ptr> errs(ndevices_);
+    std::vector<std::thread> th;
+    for (int e = 0; e < ndevices_; ++e)
+      if (owner[e] < 0)
+        th.emplace_back([&, e] {
+          try {
+            devs_[(size_t)e * inflight_] = std::make_unique<DevicePipeline>(devs[e], z, part, nparts);
+          } catch (...) {
+            errs[e] = std::current_exception();
+          }
+        });
+    for (auto& t : th) t.join();
+    for (auto& x : errs)
+      if (x) std::rethrow_exception(x);
+  }
+  for (int e = 0; e < ndevices_; ++e) {
+    const DevicePipeline* first = devs_[(size_t)(owner[e] < 0 ? e : owner[e]) * inflight_].get();
+    if (owner[e] >= 0) devs_[(size_t)e * inflight_] = std::make_unique<DevicePipeline>(devs[e], z, part, nparts, first);
+    for (int k = 1; k < inflight_; ++k)
+      devs_[(size_t)e * inflight_ + k] = std::make_unique<DevicePipeline>(devs[e], z, part, nparts, first);
   }
   // test hook: pipeline ZKP_TEST_FAIL_PIPELINE reports a device failure after
   // ZKP_TEST_FAIL_AFTER proofs (exercises the batch re-queue; never set in production)
@@ -828,6 +858,16 @@ DevicePipeline& Prover::pick_device() {
 }
 
 Prover::~Prover() = default;
+
+// a HIP error on one pipeline retires every pipeline of its device: the error may be sticky
+// device state that the ZKP_INFLIGHT siblings share
+// (a logical device = one entry of the device list and its inflight_ pipelines)
+void Prover::retire_device(const DevicePipeline& failed) {
+  size_t at = 0;
+  while (at < devs_.size() && devs_[at].get() != &failed) ++at;
+  const size_t first = at / inflight_ * inflight_;
+  for (size_t i = first; i < first + inflight_ && i < devs_.size(); ++i) devs_[i]->mark_failed();
+}
 
 // snarkjs groth16_prove's blinding, in two phases: everything but piH
 // (assemble_pre: runs while the H MSM is still on the device) and C + piH + the encoding.
@@ -996,7 +1036,7 @@ void Prover::prove(const uint8_t* wtns, size_t len, const uint8_t* r32, const ui
   try {
     m = d.prove(w, [&](const DevicePipeline::MsmOut& o) { bl = assemble_pre(hdr_, o, r32, s32); });
   } catch (const HipError&) {
-    d.mark_failed();
+    retire_device(d);
     throw;
   }
   auto t1 = std::chrono::steady_clock::now();
@@ -1065,7 +1105,7 @@ zkp_status Prover::prove_batch(const uint8_t* const* wtns, const size_t* lens, i
         assemble_post(hdr_, bl, m.h, w, &outs[i]);
         finish(i, ZKP_OK, "");
       } catch (const HipError& e) {
-        d.mark_failed();
+        retire_device(d);  // every pipeline of that device (ZKP_INFLIGHT siblings share its state)
         std::lock_guard<std::mutex> lk(qm);
         if (live_devices() > 0) {
           q.push_front(i);  // re-queue on a healthy device
@@ -1120,12 +1160,19 @@ void Prover::timings(float* ms, int n) const {
   for (int i = 0; i < n && i < 8; ++i) ms[i] = last_ms_[i];
 }
 
+DevicePipeline& Prover::staged_pipeline(int dev_index) const {
+  if (dev_index < 0 || dev_index >= ndevices_)
+    throw ZkpError(ZKP_ERR_INVALID_ARG, "device index " + std::to_string(dev_index) + " out of range (the prover has " +
+                                            std::to_string(ndevices_) + " devices)");
+  return *devs_[(size_t)dev_index * inflight_];
+}
+
 void Prover::stage(int dev, int slot, const uint8_t* wtns, size_t len) {
-  if (dev < 0 || dev >= (int)devs_.size()) throw ZkpError(ZKP_ERR_INVALID_ARG, "device index out of range");
+  DevicePipeline& d = staged_pipeline(dev);
   WtnsView w = check_wtns(hdr_, wtns, len);
-  devs_[dev]->stage(slot, w);
+  d.stage(slot, w);
   std::lock_guard<std::mutex> lk(smu_);
-  if (staged_pub_.size() < devs_.size()) staged_pub_.resize(devs_.size());
+  if (staged_pub_.size() < (size_t)ndevices_) staged_pub_.resize(ndevices_);
   auto& v = staged_pub_[dev];
   if ((size_t)slot >= v.size()) v.resize(slot + 1);
   v[slot].assign(w.values, w.values + (size_t)(hdr_.n_public + 1) * 32);
@@ -1133,10 +1180,10 @@ void Prover::stage(int dev, int slot, const uint8_t* wtns, size_t len) {
 
 void Prover::prove_staged(int dev, int slot, const uint8_t* r32, const uint8_t* s32, zkp_proof* out) {
   require_full();
-  if (dev < 0 || dev >= (int)devs_.size()) throw ZkpError(ZKP_ERR_INVALID_ARG, "device index out of range");
+  DevicePipeline& d = staged_pipeline(dev);
   auto t0 = std::chrono::steady_clock::now();
   Blinded bl;
-  DevicePipeline::MsmOut m = devs_[dev]->prove_staged(
+  DevicePipeline::MsmOut m = d.prove_staged(
       slot, [&](const DevicePipeline::MsmOut& o) { bl = assemble_pre(hdr_, o, r32, s32); });
   auto t1 = std::chrono::steady_clock::now();
   WtnsView w;

@@ -92,7 +92,8 @@ class Prover {
   // per-kernel HIP-event statistics of the bucket-accumulate kernels
   void set_instrument(bool on);
   void kernel_stats(double* out, int n) const;
-  int device_count() const { return (int)devs_.size(); }
+  int device_count() const { return ndevices_; }  // entries of the `devices` list
+  int pipelines_per_device() const { return inflight_; }
   // point-range split of one proof: this slice's MSM partial sums
   void prove_partial(const uint8_t* wtns, size_t len, zkp_partial* out);
   void prove_partial_staged(int slot, zkp_partial* out);
@@ -110,7 +111,11 @@ class Prover {
   DevicePipeline& pick_device();
   ZkeyHeader hdr_;
   int part_ = 0, nparts_ = 1;
+  int inflight_ = 1, ndevices_ = 0;
+  // inflight_ consecutive pipelines per entry of the device list (ZKP_INFLIGHT)
   std::vector<std::unique_ptr<DevicePipeline>> devs_;
+  DevicePipeline& staged_pipeline(int dev_index) const;
+  void retire_device(const DevicePipeline& failed);
   std::vector<std::vector<std::vector<uint8_t>>> staged_pub_;  // [dev][slot] -> first (nPub+1)*32 witness bytes
   mutable std::mutex smu_;
   std::atomic<unsigned> rr_{0};
@@ -145,9 +150,10 @@ struct MsmBench {
 };
 MsmBench bench_msm(int device, Curve curve, const uint8_t* points, const uint8_t* scalars, size_t n, int warmup,
                    int iters, uint8_t* out, int* is_inf);
+// ms per coset_extend (iNTT + coset key + NTT) of 2^log_n Fr elements
 float bench_ntt(int device, int log_n, int warmup, int iters);
 // ms per MsmPlan::build (digits + bucket grouping + task offsets) of n scalars, window bits c (0 = auto),
 // dense (every digit an entry: the H plan) or compacted
-float bench_plan(int device, const uint8_t* scalars, size_t n, int c, int dense, int warmup, int iters);  // ms per coset_extend (iNTT + coset + NTT)
+float bench_plan(int device, const uint8_t* scalars, size_t n, int c, int dense, int warmup, int iters);
 
 }  // namespace zkp
