@@ -168,11 +168,34 @@ zkp_status zkp_proof_calldata(const zkp_proof* proof, char* buf, size_t cap, siz
 
 /* Per-stage device timings (ms) of the last zkp_prove on this handle:
  * [0] wtns H2D, [1] buildABC, [2] NTT/quotient, [3] MSM G1 A,B1,C (own stream, overlaps
- * [1]-[2]), [4] MSM G2 B2 (own stream), [5] host assembly, [6] total wall, [7] MSM G1 H.
+ * [1]-[2]), [4] MSM G2 B2 (own stream), [5] host assembly, [6] total wall, [7] MSM G1 H,
+ * [8] verify-before-return (host; 0 when off).
  * n = capacity of ms (entries beyond n are not written). */
 zkp_status zkp_prover_timings(const zkp_prover* p, float* ms, int n);
 
 void zkp_prover_free(zkp_prover* p);
+
+/* Verify-before-return (the reference verifies every proof right after proving:
+ * dizkus-scripts/5_gen_proof.sh:14-21 `snarkjs groth16 verify`).  on != 0: every proof of
+ * zkp_prove / zkp_prove_batch[_status] / zkp_prove_staged / zkp_prove_files is checked on the
+ * host (optimal-ate pairing, the Verifier.sol:340-358 equation) against the zkey's verification
+ * key before it is returned; a proof that fails the check is never returned: the call reports
+ * ZKP_ERR_INTERNAL ("proof failed verify-before-return ...").  Default: off, or on when the
+ * environment holds ZKP_VERIFY=1 at load.  Cost: a few ms of one host core per proof (batch:
+ * on the worker thread, overlapping the next proof). */
+zkp_status zkp_prover_set_verify(zkp_prover* p, int on);
+
+/* Host only (no device): `snarkjs groth16 verify` of one proof against a zkey's verification key
+ * (sections 2 and 3).  *valid = 1 if the proof verifies (public signals from proof->public_signals,
+ * each < r), else 0; the status reports only malformed input. */
+zkp_status zkp_proof_verify(const uint8_t* zkey, size_t len, const zkp_proof* proof, int* valid);
+
+/* Host only: the BN254 optimal-ate pairing e(P, Q) as snarkjs reports GT elements (ffjavascript's
+ * final exponentiation), e.g. vk_alphabeta_12 = e(vk_alpha_1, vk_beta_2) of a verification key.
+ * g1: x, y (64 bytes), g2: x.c0, x.c1, y.c0, y.c1 (128 bytes), standard-form LE, all-zero =
+ * infinity.  out: 12 x 32 bytes, the Fq12 coefficients in snarkjs' JSON nesting order
+ * [[c0.c0, c0.c1, c0.c2], [c1.c0, c1.c1, c1.c2]], each Fq2 as (c0, c1). */
+zkp_status zkp_pairing(const uint8_t* g1, const uint8_t* g2, uint8_t* out384);
 
 /* Thread-local message of the last failing call on this thread ("" if none). */
 const char* zkp_last_error(void);

@@ -15,6 +15,7 @@
 #include "beacon.hpp"
 #include "hip_check.hpp"
 #include "host_ec.hpp"
+#include "host_pairing.hpp"
 #include "prover.hpp"
 #include "zkey_io.hpp"
 
@@ -341,6 +342,72 @@ void zkp_prover_free(zkp_prover* p) {
   if (!p) return;
   delete p->impl;
   delete p;
+}
+
+zkp_status zkp_prover_set_verify(zkp_prover* p, int on) {
+  if (!p || !p->impl) return fail(ZKP_ERR_INVALID_ARG, "null prover");
+  return guard([&] { p->impl->set_verify(on != 0); });
+}
+
+namespace {
+using zkp::host::Affine;
+using HFq = zkp::host::Fq;
+using HFq2 = zkp::host::Fq2;
+HFq fq_std(const uint8_t* b) {
+  const zkp::host::U256 v = zkp::host::u256_from_le(b);
+  if (zkp::host::u256_geq(v, zkp::host::FQ_DESC.mod)) throw zkp::ZkpError(ZKP_ERR_INVALID_ARG, "coordinate >= p");
+  return HFq::from_std(v);
+}
+bool all_zero(const uint8_t* b, size_t n) {
+  for (size_t i = 0; i < n; ++i)
+    if (b[i]) return false;
+  return true;
+}
+Affine<HFq> g1_std(const uint8_t* b) {
+  if (all_zero(b, 64)) return Affine<HFq>{HFq::zero(), HFq::zero(), true};
+  return Affine<HFq>{fq_std(b), fq_std(b + 32), false};
+}
+Affine<HFq2> g2_std(const uint8_t* b) {
+  if (all_zero(b, 128)) return Affine<HFq2>{HFq2::zero(), HFq2::zero(), true};
+  return Affine<HFq2>{HFq2{fq_std(b), fq_std(b + 32)}, HFq2{fq_std(b + 64), fq_std(b + 96)}, false};
+}
+}  // namespace
+
+zkp_status zkp_proof_verify(const uint8_t* zkey, size_t len, const zkp_proof* proof, int* valid) {
+  if (!zkey || !proof || !valid) return fail(ZKP_ERR_INVALID_ARG, "null argument");
+  return guard([&] {
+    *valid = 0;
+    const zkp::ZkeyParsed z = zkp::parse_zkey(zkey, len, false);
+    const zkp::ZkeyHeader& h = z.hdr;
+    if (h.ic.size() != (size_t)h.n_public + 1) throw zkp::ZkpError(ZKP_ERR_FORMAT, "zkey: no IC section");
+    if (proof->n_public != h.n_public || proof->public_capacity < h.n_public || (h.n_public && !proof->public_signals))
+      throw zkp::ZkpError(ZKP_ERR_INVALID_ARG, "proof: public signals do not match the key's nPublic");
+    zkp::host::VerifyingKey vk;
+    vk.alpha1 = h.alpha1, vk.beta2 = h.beta2, vk.gamma2 = h.gamma2, vk.delta2 = h.delta2;
+    vk.ic = h.ic.data();
+    vk.n_public = (int)h.n_public;
+    std::vector<zkp::host::U256> pub(h.n_public);
+    for (uint32_t i = 0; i < h.n_public; ++i) pub[i] = zkp::host::u256_from_le(proof->public_signals + 32 * (size_t)i);
+    const Affine<HFq> a = g1_std(proof->pi_a[0]), c = g1_std(proof->pi_c[0]);
+    const Affine<HFq2> b = g2_std(proof->pi_b[0][0]);
+    *valid = zkp::host::groth16_verify(vk, pub.data(), a, b, c) ? 1 : 0;
+  });
+}
+
+zkp_status zkp_pairing(const uint8_t* g1, const uint8_t* g2, uint8_t* out384) {
+  if (!g1 || !g2 || !out384) return fail(ZKP_ERR_INVALID_ARG, "null argument");
+  return guard([&] {
+    const Affine<HFq> p = g1_std(g1);
+    const Affine<HFq2> q = g2_std(g2);
+    if (!zkp::host::g1_on_curve(p) || !zkp::host::g2_on_curve(q))
+      throw zkp::ZkpError(ZKP_ERR_INVALID_ARG, "pairing: point not on the curve");
+    const zkp::host::Fq12 f = zkp::host::pairing(p, q);
+    const HFq2* c[6] = {&f.c0.c0, &f.c0.c1, &f.c0.c2, &f.c1.c0, &f.c1.c1, &f.c1.c2};
+    for (int i = 0; i < 6; ++i) {
+      zkp::host::u256_to_le(c[i]->c0.to_std(), out384 + 64 * i);
+      zkp::host::u256_to_le(c[i]->c1.to_std(), out384 + 64 * i + 32);
+    }
+  });
 }
 
 const char* zkp_last_error(void) { return g_err.c_str(); }

@@ -327,6 +327,11 @@ __device__ __forceinline__ bool hs_tile(const uint32_t* __restrict__ binbase, co
 }
 
 // hist2[(toff[b] * nsub) + sub * nt_b + t]: entries of tile t of bin b in sub-bin `sub`
+// (sub = (key >> b3) & (nsub - 1)).  AGG: wave-aggregated LDS claims (lds_claim), for skewed
+// keys where whole waves hit one counter (the witness plan's bucket of every value 1).
+// The same kernel is pass C of the tiled variant (tiles of sub-bins, b3 = 0, nsub = buckets per
+// sub-bin).
+template <bool AGG>
 __global__ __launch_bounds__(HS_TPB) void k_hs_count2(const uint2* __restrict__ ent,
                                                       const uint32_t* __restrict__ binbase,
                                                       const uint32_t* __restrict__ toff, uint32_t nbins, int b3,
@@ -336,7 +341,15 @@ __global__ __launch_bounds__(HS_TPB) void k_hs_count2(const uint2* __restrict__ 
   if (!hs_tile(binbase, toff, nbins, blockIdx.x, r)) return;
   for (uint32_t s = threadIdx.x; s < nsub; s += HS_TPB) h[s] = 0;
   __syncthreads();
-  for (uint32_t j = r.lo + threadIdx.x; j < r.hi; j += HS_TPB) atomicAdd(&h[(ent[j].x >> b3) & (nsub - 1)], 1u);
+  if (AGG) {
+    for (uint32_t j0 = r.lo; j0 < r.hi; j0 += HS_TPB) {  // whole waves iterate (lds_claim ballots)
+      const uint32_t j = j0 + threadIdx.x;
+      const bool ok = j < r.hi;
+      (void)lds_claim(h, ok ? (ent[j].x >> b3) & (nsub - 1) : 0u, ok);
+    }
+  } else {
+    for (uint32_t j = r.lo + threadIdx.x; j < r.hi; j += HS_TPB) atomicAdd(&h[(ent[j].x >> b3) & (nsub - 1)], 1u);
+  }
   __syncthreads();
   const size_t base = (size_t)toff[r.b] * nsub + r.t;
   for (uint32_t s = threadIdx.x; s < nsub; s += HS_TPB) hist2[base + (size_t)s * r.nt] = h[s];
@@ -358,11 +371,14 @@ __global__ __launch_bounds__(HS_TPB) void k_hs_subbase(const uint32_t* __restric
   subbase[q] = nt ? off2[(size_t)toff[b] * nsub + (size_t)s * nt] : binbase[b];
 }
 
+// AGG as in k_hs_count2; VALS: write only the base|sign words (.y) to vout (pass C of the tiled
+// variant: the bucket-ordered vals the accumulation reads), else the whole entries to out
+template <bool AGG, bool VALS>
 __global__ __launch_bounds__(HS_TPB) void k_hs_scatter2(const uint2* __restrict__ ent,
                                                         const uint32_t* __restrict__ binbase,
                                                         const uint32_t* __restrict__ toff, uint32_t nbins, int b3,
                                                         uint32_t nsub, const uint32_t* __restrict__ off2,
-                                                        uint2* __restrict__ out) {
+                                                        uint2* __restrict__ out, uint32_t* __restrict__ vout) {
   constexpr int NS = 1 << HS_MAX_B2;
   __shared__ uint32_t cnt[NS], off[NS], cur[NS], gbase[NS];
   __shared__ uint2 stage[HS_TILE];
@@ -379,8 +395,13 @@ __global__ __launch_bounds__(HS_TPB) void k_hs_scatter2(const uint2* __restrict_
     e[p] = j < r.hi ? ent[j] : make_uint2(0u, 0u);
   }
 #pragma unroll
-  for (int p = 0; p < PT; ++p)
-    if (r.lo + p * HS_TPB + threadIdx.x < r.hi) atomicAdd(&cnt[(e[p].x >> b3) & (nsub - 1)], 1u);
+  for (int p = 0; p < PT; ++p) {
+    const bool ok = r.lo + p * HS_TPB + threadIdx.x < r.hi;
+    if (AGG)
+      (void)lds_claim(cnt, (e[p].x >> b3) & (nsub - 1), ok);
+    else if (ok)
+      atomicAdd(&cnt[(e[p].x >> b3) & (nsub - 1)], 1u);
+  }
   __syncthreads();
   const size_t base = (size_t)toff[r.b] * nsub + r.t;
   for (uint32_t s = threadIdx.x; s < nsub; s += HS_TPB) off[s] = cnt[s];
@@ -392,13 +413,72 @@ __global__ __launch_bounds__(HS_TPB) void k_hs_scatter2(const uint2* __restrict_
   }
   __syncthreads();
 #pragma unroll
-  for (int p = 0; p < PT; ++p)
-    if (r.lo + p * HS_TPB + threadIdx.x < r.hi) stage[atomicAdd(&cur[(e[p].x >> b3) & (nsub - 1)], 1u)] = e[p];
+  for (int p = 0; p < PT; ++p) {
+    const bool ok = r.lo + p * HS_TPB + threadIdx.x < r.hi;
+    if (AGG) {
+      const uint32_t slot = lds_claim(cur, (e[p].x >> b3) & (nsub - 1), ok);
+      if (ok) stage[slot] = e[p];
+    } else if (ok) {
+      stage[atomicAdd(&cur[(e[p].x >> b3) & (nsub - 1)], 1u)] = e[p];
+    }
+  }
   __syncthreads();
   for (uint32_t j = threadIdx.x; j < r.hi - r.lo; j += HS_TPB) {
     const uint2 x = stage[j];
-    out[gbase[(x.x >> b3) & (nsub - 1)] + j] = x;
+    if (VALS)
+      vout[gbase[(x.x >> b3) & (nsub - 1)] + j] = x.y;
+    else
+      out[gbase[(x.x >> b3) & (nsub - 1)] + j] = x;
   }
+}
+
+// ---------------------------------------------------------------- pass C, tiled variant
+// For plans whose sub-bins can hold millions of entries (the compacted witness plan: every
+// witness value 1 is a digit of bucket 0; the H plan's deep low buckets) pass C is pass B again
+// one level down: every sub-bin cut into tiles of HS_TILE entries, per (sub-bin, bucket, tile)
+// counts (k_hs_count2<true>, b3 = 0) whose flat exclusive scan is every run's final position,
+// the tiles staged in LDS and written as bucket runs of base|sign words (k_hs_scatter2<true,
+// true>), then the bucket bounds and task counts (k_hs_bounds3).  No workgroup takes more than
+// HS_TILE entries whatever the skew.
+// toff3[q] = tiles of sub-bins < q (toff3[nq] = all); one workgroup
+__global__ __launch_bounds__(SC_TPB) void k_hs_subtiles(const uint32_t* __restrict__ subbase, uint32_t nq,
+                                                        uint32_t* __restrict__ toff3) {
+  __shared__ uint32_t sh[SC_TPB / 64];
+  uint32_t carry = 0;
+  for (uint32_t j0 = 0; j0 < nq; j0 += SC_TPB) {
+    const uint32_t j = j0 + threadIdx.x;
+    const uint32_t v = j < nq ? (subbase[j + 1] - subbase[j] + HS_TILE - 1) / HS_TILE : 0u;
+    uint32_t tot;
+    const uint32_t e = block_excl_scan<SC_TPB>(v, sh, tot);
+    if (j < nq) toff3[j] = carry + e;
+    carry += tot;
+  }
+  if (threadIdx.x == 0) toff3[nq] = carry;
+}
+// bucket k = (q << b3) + f: [start, end) from the scanned (sub-bin, bucket, tile) counts, task
+// counts ceil(len / S), cnt[nb] = 0
+__global__ __launch_bounds__(HS_TPB) void k_hs_bounds3(const uint32_t* __restrict__ toff3,
+                                                       const uint32_t* __restrict__ off3,
+                                                       const uint32_t* __restrict__ subbase, int b3, uint32_t nb,
+                                                       uint32_t S, uint32_t* __restrict__ start,
+                                                       uint32_t* __restrict__ end, uint32_t* __restrict__ cnt) {
+  const uint32_t k = blockIdx.x * HS_TPB + threadIdx.x;
+  if (k > nb) return;
+  if (k == nb) {
+    cnt[nb] = 0;
+    return;
+  }
+  const uint32_t nf = 1u << b3, q = k >> b3, f = k & (nf - 1);
+  const uint32_t nt = toff3[q + 1] - toff3[q];
+  uint32_t s = subbase[q], e = subbase[q];
+  if (nt) {
+    const size_t base = (size_t)toff3[q] * nf;
+    s = off3[base + (size_t)f * nt];
+    e = f + 1 < nf ? off3[base + (size_t)(f + 1) * nt] : subbase[q + 1];
+  }
+  start[k] = s;
+  end[k] = e;
+  cnt[k] = (e - s + S - 1) / S;
 }
 
 // ---------------------------------------------------------------- pass C: sub-bins -> buckets

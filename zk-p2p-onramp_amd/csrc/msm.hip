@@ -592,8 +592,19 @@ MsmPlan::MsmPlan(size_t max_n, const MsmParams& prm, hipStream_t stream)
     const char* e = std::getenv("ZKP_H_SORT");
     use_hsort_ = prm_.windows <= HS_STAGE / HS_TPB && b1 <= HS_MAX_B1 && hs_b2_ <= HS_MAX_B2 &&
                  !(e && std::string(e) == "rocprim");
+    const char* ew = std::getenv("ZKP_W_SORT");
+    use_wsort_ = use_hsort_ && !(ew && std::string(ew) == "rocprim");
+    const char* et = std::getenv("ZKP_HS_TILED_C");
+    hs_tiled_c_ = et && std::atoi(et) == 1;
+    const uint32_t nq = hs_nbins_ << hs_b2_;
+    hs_max_tiles3_ = (uint32_t)((max_entries_ + HS_TILE - 1) / HS_TILE + nq);
     size_t scan_n = nbuckets_ + 1;
     if (use_hsort_) {
+      const size_t nh3 = ((size_t)hs_max_tiles3_ << hs_b3_) + 1;
+      HIPX(hipMalloc(&hs_toff3_, ((size_t)nq + 1) * 4));
+      HIPX(hipMalloc(&hs_hist3_, nh3 * 4));
+      HIPX(hipMalloc(&hs_off3_, nh3 * 4));
+      scan_n = std::max(scan_n, nh3);
       const size_t nh = (size_t)hs_nbins_ * hs_nblk_, nh2 = (size_t)hs_max_tiles_ << hs_b2_;
       HIPX(hipMalloc(&hs_hist_, nh * 4));
       HIPX(hipMalloc(&hs_blkoff_, nh * 4));
@@ -635,7 +646,7 @@ MsmPlan::~MsmPlan() {
                   (void*)hoff_, (void*)nch_, (void*)choff_, (void*)hist2_, (void*)hoff2_, (void*)hs_hist_,
                   (void*)hs_blkoff_, (void*)hs_bintot_, (void*)hs_binbase_, (void*)hs_toff_, (void*)hs_hist2_,
                   (void*)hs_off2_, (void*)hs_subbase_, hs_ent_a_, hs_ent_b_, (void*)tsum_, (void*)perm_,
-                  (void*)tl_hist_, (void*)tl_off_})
+                  (void*)tl_hist_, (void*)tl_off_, (void*)hs_toff3_, (void*)hs_hist3_, (void*)hs_off3_})
     if (p) (void)hipFree(p);
   if (lvl_all_) (void)hipFree(lvl_all_);
   if (lvl_tsum_) (void)hipFree(lvl_tsum_);
@@ -648,10 +659,12 @@ void MsmPlan::build(const uint32_t* scalars, size_t n) {
   const uint32_t nb = (uint32_t)nbuckets_;
   hipStream_t st = stream_;
   total_ = 0;
-  bool counted = false;  // bucket bounds and task counts already written (k_dsort_fine)
-  if (dense_ && use_hsort_ && !use_bins_) {
-    // 1+2. hand-written three-pass bucket sort (hsort_kernels.hpp); total_ = n * W bounds the
-    // nonzero digits (the accumulate grid: threads past the last task exit)
+  bool counted = false;  // bucket bounds and task counts already written (k_hs_fine / k_hs_bounds3)
+  hs_built_ = false;
+  if ((dense_ ? use_hsort_ : use_wsort_) && !use_bins_) {
+    // 1+2. hand-written three-pass LDS-staged bucket sort (hsort_kernels.hpp), zero digits dropped
+    // in pass A; total_ = n * W bounds the nonzero digits (the accumulate grid: threads past the last
+    // task exit), so nothing waits on the host; the exact count stays on the device (entries_dev)
     total_ = (uint32_t)(n * W);
     if (total_ == 0) {
       HIPX(hipMemsetAsync(bstart_, 0, (nbuckets_ + 1) * 4, st));
@@ -676,18 +689,35 @@ void MsmPlan::build(const uint32_t* scalars, size_t n) {
       const size_t tiles = ((size_t)total_ + HS_TILE - 1) / HS_TILE + hs_nbins_;
       const size_t nh2 = tiles << hs_b2_;
       HIPX(hipMemsetAsync(hs_hist2_, 0, nh2 * 4, st));
-      hipLaunchKernelGGL(k_hs_count2, dim3((unsigned)tiles), dim3(HS_TPB), 0, st, ea, hs_binbase_, hs_toff_,
-                         hs_nbins_, hs_b3_, nsub, hs_hist2_);
+      const bool skew = !dense_;  // witness plans: whole waves of one bin / sub-bin / bucket
+      hipLaunchKernelGGL((skew ? k_hs_count2<true> : k_hs_count2<false>), dim3((unsigned)tiles), dim3(HS_TPB), 0, st,
+                         ea, hs_binbase_, hs_toff_, hs_nbins_, hs_b3_, nsub, hs_hist2_);
       scan_nolookback(hs_hist2_, hs_off2_, nh2, tsum_, st);
       const uint32_t nq = hs_nbins_ * nsub;
       hipLaunchKernelGGL(k_hs_subbase, dim3(grid_for(nq + 1)), dim3(HS_TPB), 0, st, hs_off2_, hs_binbase_, hs_toff_,
                          hs_nbins_, nsub, hs_subbase_);
-      hipLaunchKernelGGL(k_hs_scatter2, dim3((unsigned)tiles), dim3(HS_TPB), 0, st, ea, hs_binbase_, hs_toff_,
-                         hs_nbins_, hs_b3_, nsub, hs_off2_, eb);
+      hipLaunchKernelGGL((skew ? k_hs_scatter2<true, false> : k_hs_scatter2<false, false>), dim3((unsigned)tiles),
+                         dim3(HS_TPB), 0, st, ea, hs_binbase_, hs_toff_, hs_nbins_, hs_b3_, nsub, hs_off2_, eb,
+                         nullptr);
       // C: sub-bins -> buckets, bounds and task counts
-      hipLaunchKernelGGL(k_hs_fine, dim3(nq), dim3(HS_FINE_TPB), 0, st, eb, hs_subbase_, nq, hs_b3_, nb,
-                         (uint32_t)prm_.S, vals_sorted_, bstart_, bend_, cnt_);
+      if (dense_ && !hs_tiled_c_) {
+        hipLaunchKernelGGL(k_hs_fine, dim3(nq), dim3(HS_FINE_TPB), 0, st, eb, hs_subbase_, nq, hs_b3_, nb,
+                           (uint32_t)prm_.S, vals_sorted_, bstart_, bend_, cnt_);
+      } else {  // tiled: pass B one level down (no workgroup takes more than HS_TILE entries)
+        const uint32_t nf = 1u << hs_b3_;
+        hipLaunchKernelGGL(k_hs_subtiles, dim3(1), dim3(SC_TPB), 0, st, hs_subbase_, nq, hs_toff3_);
+        const size_t tiles3 = ((size_t)total_ + HS_TILE - 1) / HS_TILE + nq, nh3 = tiles3 << hs_b3_;
+        HIPX(hipMemsetAsync(hs_hist3_, 0, nh3 * 4, st));
+        hipLaunchKernelGGL(k_hs_count2<true>, dim3((unsigned)tiles3), dim3(HS_TPB), 0, st, eb, hs_subbase_, hs_toff3_,
+                           nq, 0, nf, hs_hist3_);
+        scan_nolookback(hs_hist3_, hs_off3_, nh3, tsum_, st);
+        hipLaunchKernelGGL((k_hs_scatter2<true, true>), dim3((unsigned)tiles3), dim3(HS_TPB), 0, st, eb, hs_subbase_,
+                           hs_toff3_, nq, 0, nf, hs_off3_, nullptr, vals_sorted_);
+        hipLaunchKernelGGL(k_hs_bounds3, dim3(grid_for((size_t)nb + 1)), dim3(HS_TPB), 0, st, hs_toff3_, hs_off3_,
+                           hs_subbase_, hs_b3_, nb, (uint32_t)prm_.S, bstart_, bend_, cnt_);
+      }
       counted = true;
+      hs_built_ = true;
     }
   } else if (dense_ && !use_bins_) {
     // 1+2. dense digits (no compaction) and a full sort on the key bits + sentinel bit
@@ -733,7 +763,7 @@ void MsmPlan::build(const uint32_t* scalars, size_t n) {
       HIPX(hipStreamSynchronize(st));
       total_ = *h_valid_;
     }
-  } else if (n > 0) {
+  } else if (n > 0 && !use_wsort_) {
     // 1. digits, compacted: only nonzero digits, window-major, point order within a window
     const uint32_t nblk = grid_for(n);
     hipLaunchKernelGGL(k_digit_count, dim3(nblk), dim3(TPB), 0, st, scalars, (uint32_t)n, prm_.c, (int)W, bcnt_);
@@ -746,7 +776,7 @@ void MsmPlan::build(const uint32_t* scalars, size_t n) {
     HIPX(hipStreamSynchronize(st));  // the sort needs the entry count on the host
     total_ = *h_valid_;
   }
-  const bool compacted = !use_bins_ && !dense_;
+  const bool compacted = !use_bins_ && !dense_ && !hs_built_ && !(use_wsort_ && n == 0);
   if (compacted) {
     HIPX(hipMemsetAsync(bstart_, 0, (nbuckets_ + 1) * 4, st));
     HIPX(hipMemsetAsync(bend_, 0, (nbuckets_ + 1) * 4, st));
@@ -811,7 +841,7 @@ MsmEngine::MsmEngine(Curve curve, const MsmParams& prm, size_t max_n, hipStream_
     HIPX(hipEventCreate(&e[0]));
     HIPX(hipEventCreate(&e[1]));
   }
-  HIPX(hipHostMalloc(&h_counts_, MAX_PENDING * 4, hipHostMallocDefault));
+  HIPX(hipHostMalloc(&h_counts_, 2 * MAX_PENDING * 4, hipHostMallocDefault));
 }
 
 MsmEngine::~MsmEngine() {
@@ -831,7 +861,7 @@ void MsmEngine::collect(Stats& s) {
     HIPX(hipEventElapsedTime(&ms, ev_[i][0], ev_[i][1]));
     s.accumulate_ms += ms;
     s.launches += 1;
-    s.mixed_adds += h_total_[i];
+    s.mixed_adds += h_total_dev_[i] ? h_counts_[MAX_PENDING + i] : h_total_[i];
     s.tasks += h_counts_[i];
   }
   pending_ = 0;
@@ -853,7 +883,10 @@ void MsmEngine::accumulate(const MsmPlan& plan, const MsmBases& bases) {
   else
     run_accumulate<Fq2>(plan, bases, part_a_, stream_, e0, e1);
   if (slot >= 0) {
-    h_total_[slot] = plan.entries();  // every compacted entry is one mixed addition
+    h_total_[slot] = plan.entries();  // every nonzero digit is one mixed addition
+    h_total_dev_[slot] = plan.entries_dev() != nullptr;
+    if (h_total_dev_[slot])  // hand-sorted plans: the exact count, not the grid bound n * W
+      HIPX(hipMemcpyAsync(&h_counts_[MAX_PENDING + slot], plan.entries_dev(), 4, hipMemcpyDeviceToHost, stream_));
     HIPX(hipMemcpyAsync(&h_counts_[slot], plan.task_off() + plan.params().buckets(), 4, hipMemcpyDeviceToHost,
                         stream_));
   }

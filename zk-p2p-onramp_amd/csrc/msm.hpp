@@ -149,7 +149,11 @@ class MsmPlan {
   hipStream_t stream() const { return stream_; }
   size_t n() const { return n_; }
   size_t max_n() const { return max_n_; }
-  uint32_t entries() const { return total_; }  // nonzero digits = mixed additions per MSM
+  // entries the accumulate grid is sized for: the nonzero digits, or for the hand-sorted plans (whose
+  // count stays on the device: no host round trip) the bound n * W
+  uint32_t entries() const { return total_; }
+  // device word holding the exact nonzero-digit count once ready() (hand-sorted plans), else nullptr
+  const uint32_t* entries_dev() const { return hs_built_ ? hs_binbase_ + hs_nbins_ : nullptr; }
   int merge_levels() const { return merge_levels_; }
 
   // device results (read-only once ready())
@@ -188,6 +192,12 @@ class MsmPlan {
   // dense plans: the hand-written three-pass LDS-staged bucket sort (hsort_kernels.hpp);
   // ZKP_H_SORT=rocprim restores the onesweep radix sort of the sentinel-keyed digits
   bool use_hsort_ = false;
+  // compacted (witness) plans sorted by the same passes (ZKP_W_SORT=rocprim: the onesweep sort and
+  // a host round trip for the entry count), always with the tiled pass C (skewed buckets); dense
+  // plans take the one-workgroup-per-sub-bin pass C unless ZKP_HS_TILED_C=1
+  bool use_wsort_ = false, hs_tiled_c_ = false, hs_built_ = false;
+  uint32_t hs_max_tiles3_ = 0;
+  uint32_t *hs_toff3_ = nullptr, *hs_hist3_ = nullptr, *hs_off3_ = nullptr;
   int hs_b2_ = 0, hs_b3_ = 0, hs_k_ = 1;  // hs_k_: scalars per thread in pass A
   uint32_t hs_nbins_ = 0, hs_nblk_ = 0, hs_max_tiles_ = 0;
   uint32_t *hs_hist_ = nullptr, *hs_blkoff_ = nullptr, *hs_bintot_ = nullptr, *hs_binbase_ = nullptr;
@@ -252,8 +262,9 @@ class MsmEngine {
   bool instrument_ = false;
   int pending_ = 0;
   hipEvent_t ev_[MAX_PENDING][2];
-  uint32_t* h_counts_ = nullptr;  // pinned: tasks per pending run
+  uint32_t* h_counts_ = nullptr;  // pinned: tasks per pending run, then entries per pending run
   uint32_t h_total_[MAX_PENDING] = {};
+  bool h_total_dev_[MAX_PENDING] = {};  // entries copied from the device (h_counts_[MAX_PENDING + i])
 };
 
 // merge levels needed for n points with the given params (worst case: one bucket of

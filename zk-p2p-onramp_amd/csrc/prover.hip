@@ -16,6 +16,7 @@
 #include <thread>
 
 #include "hip_check.hpp"
+#include "host_pairing.hpp"
 #include "qap.hpp"
 
 namespace zkp {
@@ -322,7 +323,9 @@ class DevicePipeline {
     ntt_ = std::make_unique<NttEngine>((int)h.log_domain, s0_);
     // the witness plan (built on s2) feeds A/B1/C on s2 and B2 on s1; they overlap the
     // quotient on s0, which then plans and runs the H MSM
-    plan_w_ = std::make_unique<MsmPlan>(nv, pw, s2_);
+    // ZKP_WPLAN_HI=1: the witness plan on the high-priority finish stream s3 (ahead of its G1 finishes),
+    // so its sort passes are not starved by the quotient's NTTs on s0 (measurement knob)
+    plan_w_ = std::make_unique<MsmPlan>(nv, pw, env_int("ZKP_WPLAN_HI", 0) == 1 ? s3_ : s2_);
     plan_h_ = std::make_unique<MsmPlan>(nd, ph, s4_ ? s4_ : s0_);
     // H scalars are uniform (quotient evaluations): dense digits, so the H plan never blocks
     // its host thread and the chain quotient -> plan -> H MSM is enqueued in one go
@@ -593,6 +596,7 @@ class DevicePipeline {
         HIPX(hipSetDevice(dev_));
         HIPX(hipStreamWaitEvent(s2_, ev_[1], 0));
         HIPX(hipEventRecord(ev_[9], s2_));
+        if (plan_w_->stream() != s2_) HIPX(hipStreamWaitEvent(plan_w_->stream(), ev_[1], 0));
         plan_w_->build(d_wit + wlo_ * 8, whi_ - wlo_);
         planned.set_value();
         planned_set = true;
@@ -842,6 +846,8 @@ Prover::Prover(const uint8_t* zkey, size_t len, const std::vector<int>& devices,
   }
   // test hook: pipeline ZKP_TEST_FAIL_PIPELINE reports a device failure after
   // ZKP_TEST_FAIL_AFTER proofs (exercises the batch re-queue; never set in production)
+  verify_.store(env_int("ZKP_VERIFY", 0) == 1);
+  corrupt_h_ = env_int("ZKP_TEST_CORRUPT_H", 0) == 1;
   const int fp = env_int("ZKP_TEST_FAIL_PIPELINE", -1);
   if (fp >= 0 && fp < (int)devs_.size()) devs_[fp]->set_fault_injection(env_int("ZKP_TEST_FAIL_AFTER", 0));
 }
@@ -919,6 +925,38 @@ static void assemble_post(const ZkeyHeader& h, const Blinded& bl, const Jac<HFq>
 static void assemble(const ZkeyHeader& h, const DevicePipeline::MsmOut& m, const WtnsView& w, const uint8_t* r32,
                      const uint8_t* s32, zkp_proof* out) {
   assemble_post(h, assemble_pre(h, m, r32, s32), m.h, w, out);
+}
+
+// test hook ZKP_TEST_CORRUPT_H: the H MSM result off by one generator, as a silent device error would
+static Jac<HFq> maybe_corrupt(const Jac<HFq>& h, bool on) {
+  if (!on) return h;
+  const Affine<HFq> g{HFq::one(), HFq::one() + HFq::one(), false};  // (1, 2)
+  return host::jac_add(h, host::jac_from_aff(g));
+}
+
+float Prover::verify_or_throw(const WtnsView& w, const zkp_proof* out) const {
+  const auto t0 = std::chrono::steady_clock::now();
+  if (hdr_.ic.size() != (size_t)hdr_.n_public + 1)
+    throw ZkpError(ZKP_ERR_FORMAT, "verify: the zkey has no IC section (nPublic + 1 points)");
+  host::VerifyingKey vk;
+  vk.alpha1 = hdr_.alpha1;
+  vk.beta2 = hdr_.beta2;
+  vk.gamma2 = hdr_.gamma2;
+  vk.delta2 = hdr_.delta2;
+  vk.ic = hdr_.ic.data();
+  vk.n_public = (int)hdr_.n_public;
+  std::vector<U256> pub(hdr_.n_public);
+  for (uint32_t i = 0; i < hdr_.n_public; ++i) pub[i] = host::u256_from_le(w.values + 32 * (size_t)(i + 1));
+  auto fq = [](const uint8_t* b) { return HFq::from_std(host::u256_from_le(b)); };
+  const Affine<HFq> a{fq(out->pi_a[0]), fq(out->pi_a[1]), false};
+  const Affine<HFq2> b{HFq2{fq(out->pi_b[0][0]), fq(out->pi_b[0][1])}, HFq2{fq(out->pi_b[1][0]), fq(out->pi_b[1][1])},
+                       false};
+  const Affine<HFq> c{fq(out->pi_c[0]), fq(out->pi_c[1]), false};
+  if (!host::groth16_verify(vk, pub.data(), a, b, c))
+    throw ZkpError(ZKP_ERR_INTERNAL,
+                   "proof failed verify-before-return (pairing check against the zkey's verification key): not "
+                   "returned; the device result is suspect");
+  return std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
 
 static WtnsView check_wtns(const ZkeyHeader& h, const uint8_t* wtns, size_t len) {
@@ -1040,13 +1078,15 @@ void Prover::prove(const uint8_t* wtns, size_t len, const uint8_t* r32, const ui
     throw;
   }
   auto t1 = std::chrono::steady_clock::now();
-  assemble_post(hdr_, bl, m.h, w, out);
+  assemble_post(hdr_, bl, maybe_corrupt(m.h, corrupt_h_), w, out);
   auto t2 = std::chrono::steady_clock::now();
+  const float vms = verify() ? verify_or_throw(w, out) : 0.f;
   std::lock_guard<std::mutex> lk(tmu_);
   for (int i = 0; i < 5; ++i) last_ms_[i] = m.ms[i];
   last_ms_[7] = m.ms[5];
   last_ms_[5] = std::chrono::duration<float, std::milli>(t2 - t1).count();
   last_ms_[6] = std::chrono::duration<float, std::milli>(t2 - t0).count();
+  last_ms_[8] = vms;
 }
 
 // Batch scheduler: a shared queue of witness indices; two
@@ -1102,7 +1142,8 @@ zkp_status Prover::prove_batch(const uint8_t* const* wtns, const size_t* lens, i
         DevicePipeline::MsmOut m = d.prove(w, [&](const DevicePipeline::MsmOut& o) {
           bl = assemble_pre(hdr_, o, r32s ? r32s[i] : nullptr, s32s ? s32s[i] : nullptr);
         });
-        assemble_post(hdr_, bl, m.h, w, &outs[i]);
+        assemble_post(hdr_, bl, maybe_corrupt(m.h, corrupt_h_), w, &outs[i]);
+        if (verify()) verify_or_throw(w, &outs[i]);  // on the worker thread: overlaps the next proof
         finish(i, ZKP_OK, "");
       } catch (const HipError& e) {
         retire_device(d);  // every pipeline of that device (ZKP_INFLIGHT siblings share its state)
@@ -1157,7 +1198,7 @@ void Prover::quotient(const uint8_t* wtns, size_t len, uint8_t* out) {
 
 void Prover::timings(float* ms, int n) const {
   std::lock_guard<std::mutex> lk(tmu_);
-  for (int i = 0; i < n && i < 8; ++i) ms[i] = last_ms_[i];
+  for (int i = 0; i < n && i < 9; ++i) ms[i] = last_ms_[i];
 }
 
 DevicePipeline& Prover::staged_pipeline(int dev_index) const {
@@ -1192,13 +1233,15 @@ void Prover::prove_staged(int dev, int slot, const uint8_t* r32, const uint8_t* 
     w.values = staged_pub_[dev][slot].data();
     w.n_witness = hdr_.n_vars;
   }
-  assemble_post(hdr_, bl, m.h, w, out);
+  assemble_post(hdr_, bl, maybe_corrupt(m.h, corrupt_h_), w, out);
   auto t2 = std::chrono::steady_clock::now();
+  const float vms = verify() ? verify_or_throw(w, out) : 0.f;
   std::lock_guard<std::mutex> lk(tmu_);
   for (int i = 0; i < 5; ++i) last_ms_[i] = m.ms[i];
   last_ms_[7] = m.ms[5];
   last_ms_[5] = std::chrono::duration<float, std::milli>(t2 - t1).count();
   last_ms_[6] = std::chrono::duration<float, std::milli>(t2 - t0).count();
+  last_ms_[8] = vms;
 }
 
 void Prover::set_instrument(bool on) {

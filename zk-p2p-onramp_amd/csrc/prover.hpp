@@ -50,6 +50,7 @@ struct ZkeyHeader {
   uint32_t n_coef = 0;
   host::Affine<host::Fq> alpha1, beta1, delta1;
   host::Affine<host::Fq2> beta2, gamma2, delta2;
+  std::vector<host::Affine<host::Fq>> ic;  // section 3 (nPublic + 1 points; empty if the key has none)
 };
 
 struct WtnsView {
@@ -105,6 +106,13 @@ class Prover {
   // MSM configuration of device 0: [0] witness c, [1] witness depth, [2] witness groups,
   // [3] H c, [4] H depth, [5] H groups, [6] base-table bytes per device
   void msm_config(double* out, int n) const;
+  // verify-before-return (the reference verifies every proof after proving,
+  // dizkus-scripts/5_gen_proof.sh:14-21): every proof of zkp_prove / zkp_prove_batch /
+  // zkp_prove_staged is checked by the host pairing (host_pairing.cpp) against the zkey's
+  // verification key; a proof that fails is an error (ZKP_ERR_INTERNAL), never returned.
+  // Default: environment ZKP_VERIFY=1 at load, else off.
+  void set_verify(bool on) { verify_.store(on); }
+  bool verify() const { return verify_.load(); }
 
  private:
   void require_full() const;
@@ -120,7 +128,11 @@ class Prover {
   mutable std::mutex smu_;
   std::atomic<unsigned> rr_{0};
   mutable std::mutex tmu_;
-  float last_ms_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  float last_ms_[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};  // [8]: verify-before-return (host ms)
+  std::atomic<bool> verify_{false};
+  bool corrupt_h_ = false;  // test hook ZKP_TEST_CORRUPT_H=1: piH + G1 generator (a silent device error)
+  // throws ZkpError(ZKP_ERR_INTERNAL) unless the assembled proof verifies; returns the host ms spent
+  float verify_or_throw(const WtnsView& w, const zkp_proof* out) const;
   friend class DevicePipeline;
 };
 

@@ -132,6 +132,9 @@ ZkeyParsed parse_zkey(const uint8_t* buf, size_t len, bool with_coefs) {
   chk(7, (uint64_t)h.n_vars * 128);
   chk(8, (uint64_t)(h.n_vars - h.n_public - 1) * 64);
   chk(9, (uint64_t)h.domain_size * 64);
+  const Section& s3 = z.bf.sec[3];  // IC (the verification key's public-input points)
+  if (s3.ptr && s3.len == ((uint64_t)h.n_public + 1) * 64)
+    for (uint32_t i = 0; i <= h.n_public; ++i) h.ic.push_back(g1_from_zkey(s3.ptr + (size_t)i * 64));
   const Section& s4 = z.bf.sec[4];
   if (!s4.ptr || s4.len < 4) throw ZkpError(ZKP_ERR_FORMAT, "zkey: missing coefficients section");
   h.n_coef = rd32(s4.ptr);

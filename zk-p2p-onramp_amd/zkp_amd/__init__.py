@@ -129,7 +129,10 @@ def load_library(path: str = LIB_PATH):
                                           ctypes.POINTER(_Proof)]
         lib.zkp_quotient_part_staged.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.POINTER(P)]
         lib.zkp_prove_partial_ext_staged.argtypes = [P, ctypes.c_int, ctypes.POINTER(P), ctypes.c_char_p]
-        for name in ("zkp_prover_load_mem", "zkp_prover_load_file", "zkp_prover_info", "zkp_prove",
+        lib.zkp_prover_set_verify.argtypes = [P, ctypes.c_int]
+        lib.zkp_proof_verify.argtypes = [u8p, sz, ctypes.POINTER(_Proof), ctypes.POINTER(ctypes.c_int)]
+        lib.zkp_pairing.argtypes = [u8p, u8p, u8p]
+        for name in ("zkp_prover_set_verify", "zkp_proof_verify", "zkp_pairing", "zkp_prover_load_mem", "zkp_prover_load_file", "zkp_prover_info", "zkp_prove",
                      "zkp_prove_batch", "zkp_prove_batch_status", "zkp_prove_files", "zkp_proof_json", "zkp_public_json",
                      "zkp_prover_timings", "zkp_msm_g1", "zkp_msm_g2", "zkp_ntt_fr", "zkp_quotient",
                      "zkp_witness_stage", "zkp_prove_staged", "zkp_prover_instrument", "zkp_prover_kernel_stats",
@@ -309,11 +312,16 @@ class Prover:
 
     def timings(self):
         lib = load_library()
-        ms = (ctypes.c_float * 8)()
-        _check(lib.zkp_prover_timings(self._h, ms, 8))
+        ms = (ctypes.c_float * 9)()
+        _check(lib.zkp_prover_timings(self._h, ms, 9))
         keys = ["wtns_h2d", "build_abc", "ntt_quotient", "msm_g1_abc", "msm_g2", "host_assembly", "total_wall",
-                "msm_g1_h"]
+                "msm_g1_h", "verify"]
         return dict(zip(keys, list(ms)))
+
+    def set_verify(self, on: bool = True):
+        """Verify-before-return (zkp_prover_set_verify): every proof is checked by the host pairing
+        against the zkey's verification key; a failing proof raises ZkpError (ZKP_ERR_INTERNAL)."""
+        _check(load_library().zkp_prover_set_verify(self._h, 1 if on else 0))
 
     def stage(self, wtns: bytes, slot: int, dev_index: int = 0):
         wp, wk = _buf(wtns)
@@ -538,6 +546,50 @@ def zkey_new(r1cs: bytes, ptau: bytes, device: int = 0) -> bytes:
         return _copy_out(out, n.value)
     finally:
         lib.zkp_buffer_free(out)
+
+
+def _proof_struct(proof, public_signals):
+    (a, b, c) = proof
+    pr = _Proof()
+    for i in range(2):
+        pr.pi_a[i][:] = int(a[i]).to_bytes(32, "little")
+        pr.pi_c[i][:] = int(c[i]).to_bytes(32, "little")
+        for j in range(2):
+            pr.pi_b[i][j][:] = int(b[i][j]).to_bytes(32, "little")
+    pub = b"".join(int(x).to_bytes(32, "little") for x in public_signals) or bytes(32)
+    pbuf = (ctypes.c_uint8 * len(pub)).from_buffer_copy(pub)
+    pr.n_public = pr.public_capacity = len(public_signals)
+    pr.public_signals = ctypes.cast(pbuf, ctypes.POINTER(ctypes.c_uint8))
+    return pr, pbuf
+
+
+def proof_verify(zkey, proof, public_signals) -> bool:
+    """Host-only `snarkjs groth16 verify` (zkp_proof_verify) of a proof tuple
+    ((ax, ay), ((bx0, bx1), (by0, by1)), (cx, cy)) against a zkey's verification key."""
+    if hasattr(zkey, "ptr") and hasattr(zkey, "len"):
+        zp, zlen, zk = ctypes.cast(zkey.ptr, ctypes.POINTER(ctypes.c_uint8)), zkey.len, None
+    else:
+        zp, zk = _buf(bytes(zkey))
+        zlen = len(zkey)
+    pr, keep = _proof_struct(proof, public_signals)
+    ok = ctypes.c_int()
+    _check(load_library().zkp_proof_verify(zp, zlen, ctypes.byref(pr), ctypes.byref(ok)))
+    return bool(ok.value)
+
+
+def pairing(g1, g2):
+    """Host-only BN254 pairing e(P, Q) in snarkjs' GT convention (zkp_pairing): P = (x, y),
+    Q = ((x.c0, x.c1), (y.c0, y.c1)), None = infinity -> 6 x (c0, c1) ints in snarkjs' nesting."""
+    gb = bytes(64) if g1 is None else b"".join(int(v).to_bytes(32, "little") for v in g1)
+    qb = bytes(128) if g2 is None else b"".join(int(v).to_bytes(32, "little")
+                                               for v in (g2[0][0], g2[0][1], g2[1][0], g2[1][1]))
+    gp, gk = _buf(gb)
+    qp, qk = _buf(qb)
+    out = (ctypes.c_uint8 * 384)()
+    _check(load_library().zkp_pairing(gp, qp, ctypes.cast(out, ctypes.POINTER(ctypes.c_uint8))))
+    raw = bytes(out)
+    v = [_le(raw[32 * i:32 * i + 32]) for i in range(12)]
+    return [[(v[6 * h + 2 * k], v[6 * h + 2 * k + 1]) for k in range(3)] for h in range(2)]
 
 
 def solidity_calldata(proof, public_signals) -> str:
