@@ -88,29 +88,48 @@ zkp_status zkp_zkey_read(const char* path, uint8_t** out, size_t* len);
 zkp_status zkp_zkey_read_chunks(const char* const* paths, int n, uint8_t** out, size_t* len);
 void zkp_buffer_free(uint8_t* p);
 
-/* Setup acceleration: the group arithmetic of a phase-2 contribution (`snarkjs zkey
- * contribute` / `zkey beacon`, reference dizkus-scripts/3_gen_chunk_zkey.sh:27,36) with
+/* Setup acceleration, primitive: the group arithmetic of a phase-2 contribution with a given
  * secret k (32-byte LE, nonzero mod r) on `device`: delta1, delta2 x k (section 2), every
- * L (section 8) and H (section 9) point x k^-1.  Section 10 (the contribution
- * transcript) is copied unchanged.  *out: the new zkey (free with zkp_buffer_free). */
+ * L (section 8) and H (section 9) point x k^-1.  Section 10 (the contribution record) is
+ * copied unchanged, so the result does not pass `zkey verify`: the snarkjs commands are
+ * zkp_zkey_contribute_entropy / zkp_zkey_beacon.  *out: the new zkey (zkp_buffer_free). */
 zkp_status zkp_zkey_contribute(int device, const uint8_t* zkey, size_t len, const uint8_t* k32, uint8_t** out,
                                size_t* out_len);
 
-/* Setup acceleration: `snarkjs zkey beacon <in.zkey> <out.zkey> <beaconHashHex> <numIterationsExp>`
- * (reference dizkus-scripts/3_gen_chunk_zkey.sh:36).  zkp_beacon_secret (host only) derives the
- * contribution scalar as snarkjs@0.4.22 / ffjavascript do: 2^e chained SHA-256 of the beacon, a
- * ChaCha20 stream seeded with the hash, Fr.fromRng; k32: 32-byte LE.  zkp_zkey_beacon applies it
- * with zkp_zkey_contribute (section 10 unchanged).  e <= 63. */
+/* Setup acceleration: `snarkjs zkey beacon <in.zkey> <out.zkey> <beaconHashHex> <numIterationsExp>
+ * [-n=name]` (reference dizkus-scripts/3_gen_chunk_zkey.sh:36).  zkp_beacon_secret (host only)
+ * derives the contribution scalar as snarkjs@0.4.22 / ffjavascript do: 2^e chained SHA-256 of the
+ * beacon, a ChaCha20 stream seeded with the hash, Fr.fromRng; k32: 32-byte LE.  zkp_zkey_beacon
+ * draws the rest of the contribution from the same stream (G1.fromRng, the transcript, hashToG2),
+ * applies k on the GPU and appends the type-1 record (deltaAfter, proof of knowledge,
+ * transcript, numIterationsExp, beacon hash, name) to section 10, so the key passes `zkey
+ * verify` (reference circuit/scripts/generate_keys_phase2_groth16.sh:26).  e <= 63; name may be
+ * NULL (not recorded).  Record bytes restated (oracle/mpc.py), parity unpinned. */
 zkp_status zkp_beacon_secret(const uint8_t* beacon, size_t len, uint32_t num_iterations_exp, uint8_t* k32);
 zkp_status zkp_zkey_beacon(int device, const uint8_t* zkey, size_t len, const uint8_t* beacon, size_t beacon_len,
                            uint32_t num_iterations_exp, uint8_t** out, size_t* out_len);
+zkp_status zkp_zkey_beacon_named(int device, const uint8_t* zkey, size_t len, const uint8_t* beacon, size_t beacon_len,
+                                 uint32_t num_iterations_exp, const char* name, uint8_t** out, size_t* out_len);
+
+/* Setup acceleration: `snarkjs zkey contribute <in.zkey> <out.zkey> -e=<entropy> [-n=name]`
+ * (reference dizkus-scripts/3_gen_chunk_zkey.sh:27): the contribution's rng is ChaCha20 seeded with
+ * Blake2b-512(64 random bytes || entropy) (snarkjs misc.getRandomRng); rand64: those 64 bytes
+ * (NULL: /dev/urandom; non-NULL only for reproducible tests).  The secret and the type-0 record
+ * are drawn as for the beacon; the group arithmetic runs on `device`. */
+zkp_status zkp_zkey_contribute_entropy(int device, const uint8_t* zkey, size_t len, const uint8_t* rand64,
+                                       const char* entropy, const char* name, uint8_t** out, size_t* out_len);
+
+/* Host only: Blake2b-512 of a buffer (the hash of the MPC transcript and circuit hash; exported so
+ * the CPU tests pin it against Python's hashlib). */
+zkp_status zkp_blake2b512(const uint8_t* data, size_t len, uint8_t* out64);
 
 /* Setup acceleration: `snarkjs zkey new <circuit.r1cs> <pot.ptau> <circuit_0000.zkey>`
  * (reference dizkus-scripts/3_gen_chunk_zkey.sh:18) on `device`: the phase-2 starting key
  * (gamma = delta = 1) of a circom .r1cs (v1) from a prepared .ptau (v1, Lagrange sections 12-15,
  * power >= log2(domain) + 1).  A/B1/B2/IC/L are sparse sums of ptau Lagrange points with the
  * circuit's coefficients, built on the GPU; H is copied from the odd points of the next level.
- * Section 10 holds no contributions and a zero csHash.  *out: the zkey (zkp_buffer_free). */
+ * Section 10 holds no contributions and the circuit hash (csHash: Blake2b-512 over the key's
+ * points and the ptau's tauG1 powers, host).  *out: the zkey (zkp_buffer_free). */
 zkp_status zkp_zkey_new(int device, const uint8_t* r1cs, size_t r1cs_len, const uint8_t* ptau, size_t ptau_len,
                         uint8_t** out, size_t* out_len);
 

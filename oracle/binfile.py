@@ -154,7 +154,14 @@ def write_zkey(z: ZKey) -> bytes:
     sec7 = b"".join(bn254.g2_to_lem(p) for p in z.b2)
     sec8 = b"".join(bn254.g1_to_lem(p) for p in z.c)
     sec9 = b"".join(bn254.g1_to_lem(p) for p in z.h)
-    sec10 = bytes(64) + struct.pack("<I", 0)  # csHash + 0 contributions (prove ignores it)
+    # section 10, the MPC record (prove ignores it): z.extra["mpc"] (oracle/mpc.py) when the key
+    # carries one, else a zero csHash and no contributions
+    mpc = z.extra.get("mpc")
+    if mpc is not None:
+        from .mpc import write_mpc
+        sec10 = write_mpc(mpc)
+    else:
+        sec10 = bytes(64) + struct.pack("<I", 0)
     return write_binfile(b"zkey", 1, [(1, sec1), (2, sec2), (3, sec3), (4, sec4), (5, sec5),
                                       (6, sec6), (7, sec7), (8, sec8), (9, sec9), (10, sec10)])
 
@@ -218,8 +225,13 @@ def read_zkey(buf: bytes) -> ZKey:
     b2 = [bn254.g2_from_lem(buf[off7 + 128 * i:off7 + 128 * (i + 1)]) for i in range(n_vars)]
     c = g1s(8, n_vars - n_public - 1)
     h = g1s(9, domain)
-    return ZKey(n_vars, n_public, domain, alpha1, beta1, beta2, gamma2, delta1, delta2, ic, coefs,
-                a, b1, b2, c, h)
+    z = ZKey(n_vars, n_public, domain, alpha1, beta1, beta2, gamma2, delta1, delta2, ic, coefs,
+             a, b1, b2, c, h)
+    if 10 in secs:
+        from .mpc import read_mpc
+        off, ln = secs[10][0]
+        z.extra["mpc"] = read_mpc(buf[off:off + ln])
+    return z
 
 
 def read_zkey_vk(buf):

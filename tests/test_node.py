@@ -122,14 +122,16 @@ def test_addon_zkey_new_checks_arguments():
 def test_node_cli_zkey_new(tmp_path):
     """`cli.js zkey new|groth16 setup <r1cs> <ptau> <zkey>` (snarkjs' setup step, reference
     dizkus-scripts/3_gen_chunk_zkey.sh:18) writes the oracle's key byte for byte."""
-    from oracle import binfile, circuit, groth16, setup
+    from oracle import binfile, circuit, groth16, mpc, setup
     TAU, ALPHA, BETA = 0x1234567890ABCDEF1122334455667788 % groth16.R, 987654321987654321, 555555555555
     m = json.load(open(os.path.join(GOLD, "manifest.json")))["circuits"]["tiny"]
     r1cs, _ = circuit.gen_circuit(m["n_vars"], m["n_constraints"], m["n_public"], m["circuit_seed"])
     k = circuit.domain_size_for(r1cs.n_constraints, r1cs.n_public).bit_length() - 1
     (tmp_path / "c.r1cs").write_bytes(binfile.write_r1cs(r1cs))
     (tmp_path / "p.ptau").write_bytes(setup.ptau_known_tau(k + 1, TAU, ALPHA, BETA))
-    want = binfile.write_zkey(setup.zkey_new(r1cs, TAU, ALPHA, BETA))
+    z = setup.zkey_new(r1cs, TAU, ALPHA, BETA)
+    z.extra["mpc"] = {"cs_hash": mpc.cs_hash(z, TAU), "contributions": []}
+    want = binfile.write_zkey(z)
     for i, argv in enumerate([["zkey", "new"], ["groth16", "setup"]]):  # the reference runs `groth16 setup ... -e=`
         out = tmp_path / ("c%d.zkey" % i)
         extra = ["-e=some entropy"] if argv[0] == "groth16" else []
@@ -154,12 +156,35 @@ def test_node_zkey_beacon_checks_arguments():
 @pytest.mark.gpu
 def test_node_cli_zkey_beacon(tmp_path):
     """`cli.js zkey beacon <in> <out> <hex> 10 -n=...` (reference 3_gen_chunk_zkey.sh:36) writes the
-    oracle's contribution with the beacon's secret (oracle/beacon.py)."""
-    from oracle import beacon, binfile, setup
+    oracle's contribution with the beacon's secret (oracle/beacon.py) and its record (oracle/mpc.py)."""
+    from oracle import binfile, mpc
     zk = os.path.join(GOLD, "circuit_tiny.zkey")
     hx = "0102030405060708090a0b0c0d0e0f101112131415161718191a1b1c1d1e1f20"
     r = subprocess.run([NODE, os.path.join(JS, "cli.js"), "zkey", "beacon", zk, str(tmp_path / "b.zkey"), hx, "10",
                         "-n=Final Beacon phase2"], capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr
-    want = setup.contribute_delta(binfile.read_zkey(open(zk, "rb").read()), beacon.beacon_secret(bytes.fromhex(hx), 10))
+    want, _ = mpc.beacon(binfile.read_zkey(open(zk, "rb").read()), bytes.fromhex(hx), 10, name="Final Beacon phase2")
     assert (tmp_path / "b.zkey").read_bytes() == binfile.write_zkey(want)
+
+
+@pytest.mark.gpu
+def test_node_cli_ceremony_passes_zkey_verify(tmp_path):
+    """The reference's key ceremony through the CLI (dizkus-scripts/3_gen_chunk_zkey.sh:18,27,36:
+    `groth16 setup ... -e=`, `zkey contribute -e= -n=`, `zkey beacon $BEACON 10 -n=`); the final key
+    passes the restated `zkey verify` (circuit/scripts/generate_keys_phase2_groth16.sh:26)."""
+    from oracle import binfile, circuit, groth16, mpc, setup
+    TAU, ALPHA, BETA = 0x1234567890ABCDEF1122334455667788 % groth16.R, 987654321987654321, 555555555555
+    r1cs, _ = circuit.gen_circuit(12, 10, 2, 11)
+    k = circuit.domain_size_for(r1cs.n_constraints, r1cs.n_public).bit_length() - 1
+    (tmp_path / "c.r1cs").write_bytes(binfile.write_r1cs(r1cs))
+    (tmp_path / "p.ptau").write_bytes(setup.ptau_known_tau(k + 1, TAU, ALPHA, BETA))
+    cli = [NODE, os.path.join(JS, "cli.js")]
+    steps = [["groth16", "setup", str(tmp_path / "c.r1cs"), str(tmp_path / "p.ptau"), str(tmp_path / "k0.zkey"), "-e=x"],
+             ["zkey", "contribute", str(tmp_path / "k0.zkey"), str(tmp_path / "k1.zkey"), "-e=random text", "-n=1st"],
+             ["zkey", "beacon", str(tmp_path / "k1.zkey"), str(tmp_path / "k2.zkey"),
+              "0102030405060708090a0b0c0d0e0f101112131415161718191a1b1c1d1e1f20", "10", "-n=Final Beacon phase2"]]
+    for st in steps:
+        r = subprocess.run(cli + st, capture_output=True, text=True, timeout=600)
+        assert r.returncode == 0, r.stderr
+    ok, msg = mpc.zkey_verify((tmp_path / "k2.zkey").read_bytes(), (tmp_path / "k0.zkey").read_bytes())
+    assert ok, msg

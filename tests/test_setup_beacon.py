@@ -8,13 +8,14 @@ ChaCha block function and block counter are pinned by OpenSSL's chacha20 keystre
 hashlib; the composition has no snarkjs fixture (parity unpinned).
 CPU: the oracle against the OpenSSL vectors; the C ABI's host-only derivation
 (zkp_beacon_secret) against the oracle.
-GPU: zkp_zkey_beacon == the oracle's contribution with the beacon's secret, byte for byte."""
+GPU: zkp_zkey_beacon == the oracle's contribution with the beacon's secret, byte for byte, with
+the contribution record (oracle/mpc.py) appended to section 10."""
 import json
 import os
 
 import pytest
 
-from oracle import beacon, binfile, groth16, setup
+from oracle import beacon, binfile, groth16, mpc, setup
 import zkp_amd
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -55,8 +56,10 @@ def test_gpu_zkey_beacon_matches_oracle_and_proves(name):
     zk = open(os.path.join(GOLD, "circuit_%s.zkey" % name), "rb").read()
     wt = open(os.path.join(GOLD, "circuit_%s.wtns" % name), "rb").read()
     raw = bytes.fromhex(VEC["beacon_oracle"][0]["beacon_hex"])
-    out = zkp_amd.zkey_beacon(zk, raw, 10)
-    z2 = setup.contribute_delta(binfile.read_zkey(zk), beacon.beacon_secret(raw, 10))
-    assert out == binfile.write_zkey(z2)
+    out = zkp_amd.zkey_beacon(zk, raw, 10, name="Final Beacon phase2")
+    z2, k = mpc.beacon(binfile.read_zkey(zk), raw, 10, name="Final Beacon phase2")
+    assert k == beacon.beacon_secret(raw, 10)
+    assert z2.delta1 == setup.contribute_delta(binfile.read_zkey(zk), k).delta1
+    assert out == binfile.write_zkey(z2)  # including the type-1 record appended to section 10
     (a, b, c), pub = zkp_amd.Prover(out).prove_raw(wt)
     assert groth16.verify_with_zkey(z2, pub, {"A": a, "B": b, "C": c})

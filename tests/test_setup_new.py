@@ -9,15 +9,16 @@ independently of the known-tau setup that gives the expected key (gamma = delta 
 CPU: the two oracle paths agree where they overlap (the H section is the ptau's odd level-(k+1)
 Lagrange points; alpha1/beta1/beta2 are its first points), and a proof made with the new key
 verifies under it.
-GPU: zkp_zkey_new(r1cs, ptau) is byte-identical to the oracle's key, and the GPU prover's
-proofs with it verify."""
+GPU: zkp_zkey_new(r1cs, ptau) is byte-identical to the oracle's key -- including section 10's
+circuit hash (csHash, oracle/mpc.py; recalled snarkjs composition, parity unpinned) -- and the GPU
+prover's proofs with it verify."""
 import json
 import os
 import struct
 
 import pytest
 
-from oracle import binfile, bn254, circuit, groth16, setup
+from oracle import binfile, bn254, circuit, groth16, mpc, setup
 import zkp_amd
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -34,6 +35,8 @@ def _case(name):
         k = n.bit_length() - 1
         ptau = setup.ptau_known_tau(k + 1, TAU, ALPHA, BETA)
         z = setup.zkey_new(r1cs, TAU, ALPHA, BETA)
+        # section 10 of a new key: the circuit hash (oracle/mpc.py) and no contributions
+        z.extra["mpc"] = {"cs_hash": mpc.cs_hash(z, TAU), "contributions": []}
         _cache[name] = (r1cs, w, n, k, ptau, z)
     return _cache[name]
 

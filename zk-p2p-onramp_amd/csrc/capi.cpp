@@ -16,6 +16,7 @@
 #include "hip_check.hpp"
 #include "host_ec.hpp"
 #include "host_pairing.hpp"
+#include "mpc.hpp"
 #include "prover.hpp"
 #include "zkey_io.hpp"
 
@@ -208,16 +209,75 @@ zkp_status zkp_beacon_secret(const uint8_t* beacon, size_t len, uint32_t num_ite
   return guard([&] { zkp::beacon_secret(beacon, len, num_iterations_exp, k32); });
 }
 
-zkp_status zkp_zkey_beacon(int device, const uint8_t* zkey, size_t len, const uint8_t* beacon, size_t beacon_len,
-                           uint32_t num_iterations_exp, uint8_t** out, size_t* out_len) {
+namespace {
+// one phase-2 contribution drawn from rng: the record appended to section 10 (mpc.cpp), then the
+// group arithmetic on the GPU (delta -> k delta, L and H -> k^-1) and the new section 10
+std::vector<uint8_t> contribute_mpc(int device, const uint8_t* zkey, size_t len, zkp::ChaChaRng& rng, uint32_t type,
+                                    const char* name, const uint8_t* beacon, size_t beacon_len, uint32_t e) {
+  const zkp::ZkeyParsed z = zkp::parse_zkey(zkey, len, false);
+  const zkp::Section& s10 = z.bf.sec[10];
+  if (!s10.ptr) throw zkp::ZkpError(ZKP_ERR_FORMAT, "zkey: missing section 10 (MPC parameters)");
+  zkp::MpcParams m = zkp::read_mpc(s10.ptr, s10.len);
+  uint8_t k[32];
+  zkp::mpc_contribute(m, rng, z.hdr.delta1, type, name ? std::string(name) : std::string(), beacon, beacon_len, e, k);
+  std::vector<uint8_t> buf = zkp::zkey_apply_delta(device, zkey, len, k);
+  zkp::binfile_replace_section(buf, 10, zkp::write_mpc(m));
+  return buf;
+}
+}  // namespace
+
+zkp_status zkp_zkey_beacon_named(int device, const uint8_t* zkey, size_t len, const uint8_t* beacon, size_t beacon_len,
+                                 uint32_t num_iterations_exp, const char* name, uint8_t** out, size_t* out_len) {
   if (!zkey || (!beacon && beacon_len) || !out || !out_len) return fail(ZKP_ERR_INVALID_ARG, "null argument");
   std::vector<uint8_t> buf;
   zkp_status s = guard([&] {
-    uint8_t k[32];
-    zkp::beacon_secret(beacon, beacon_len, num_iterations_exp, k);
-    buf = zkp::zkey_apply_delta(device, zkey, len, k);
+    uint8_t h[32];
+    zkp::beacon_hash(beacon, beacon_len, num_iterations_exp, h);
+    uint32_t seed[8];
+    zkp::seed_from_hash(h, seed);
+    zkp::ChaChaRng rng(seed);
+    buf = contribute_mpc(device, zkey, len, rng, 1, name, beacon, beacon_len, num_iterations_exp);
   });
   return s != ZKP_OK ? s : hand_out(std::move(buf), out, out_len);
+}
+
+zkp_status zkp_zkey_beacon(int device, const uint8_t* zkey, size_t len, const uint8_t* beacon, size_t beacon_len,
+                           uint32_t num_iterations_exp, uint8_t** out, size_t* out_len) {
+  return zkp_zkey_beacon_named(device, zkey, len, beacon, beacon_len, num_iterations_exp, nullptr, out, out_len);
+}
+
+zkp_status zkp_zkey_contribute_entropy(int device, const uint8_t* zkey, size_t len, const uint8_t* rand64,
+                                       const char* entropy, const char* name, uint8_t** out, size_t* out_len) {
+  if (!zkey || !entropy || !out || !out_len) return fail(ZKP_ERR_INVALID_ARG, "null argument");
+  std::vector<uint8_t> buf;
+  zkp_status s = guard([&] {
+    uint8_t rnd[64];
+    if (rand64) {
+      std::memcpy(rnd, rand64, 64);
+    } else {  // snarkjs misc.getRandomRng: 64 bytes from the OS CSPRNG
+      std::ifstream f("/dev/urandom", std::ios::binary);
+      if (!f.read(reinterpret_cast<char*>(rnd), 64)) throw zkp::ZkpError(ZKP_ERR_IO, "cannot read /dev/urandom");
+    }
+    zkp::Blake2b hh;
+    hh.update(rnd, 64);
+    hh.update(entropy, std::strlen(entropy));
+    uint8_t d[64];
+    hh.final(d);
+    uint32_t seed[8];
+    zkp::seed_from_hash(d, seed);
+    zkp::ChaChaRng rng(seed);
+    buf = contribute_mpc(device, zkey, len, rng, 0, name, nullptr, 0, 0);
+  });
+  return s != ZKP_OK ? s : hand_out(std::move(buf), out, out_len);
+}
+
+zkp_status zkp_blake2b512(const uint8_t* data, size_t len, uint8_t* out64) {
+  if ((!data && len) || !out64) return fail(ZKP_ERR_INVALID_ARG, "null argument");
+  return guard([&] {
+    zkp::Blake2b h;
+    h.update(data, len);
+    h.final(out64);
+  });
 }
 
 zkp_status zkp_zkey_new(int device, const uint8_t* r1cs, size_t r1cs_len, const uint8_t* ptau, size_t ptau_len,

@@ -323,9 +323,10 @@ class DevicePipeline {
     ntt_ = std::make_unique<NttEngine>((int)h.log_domain, s0_);
     // the witness plan (built on s2) feeds A/B1/C on s2 and B2 on s1; they overlap the
     // quotient on s0, which then plans and runs the H MSM
-    // ZKP_WPLAN_HI=1: the witness plan on the high-priority finish stream s3 (ahead of its G1 finishes),
-    // so its sort passes are not starved by the quotient's NTTs on s0 (measurement knob)
-    plan_w_ = std::make_unique<MsmPlan>(nv, pw, env_int("ZKP_WPLAN_HI", 0) == 1 ? s3_ : s2_);
+    // the witness plan on the high-priority finish stream s3 (ahead of its G1 finishes), so its sort
+    // passes are not starved by the quotient's NTTs on s0: the witness accumulations start ~5 ms
+    // earlier; proof 26.69 -> 26.58 ms on one box (profiles/wplan_r03.txt; ZKP_WPLAN_HI=0: s2)
+    plan_w_ = std::make_unique<MsmPlan>(nv, pw, env_int("ZKP_WPLAN_HI", 1) == 1 ? s3_ : s2_);
     plan_h_ = std::make_unique<MsmPlan>(nd, ph, s4_ ? s4_ : s0_);
     // H scalars are uniform (quotient evaluations): dense digits, so the H plan never blocks
     // its host thread and the chain quotient -> plan -> H MSM is enqueued in one go

@@ -13,8 +13,9 @@
 // Shamir's trick (one shared doubling chain over the scalars' bits, one mixed addition per set
 // bit, on the prover's field/curve code), its partials summed per point, then affine and back to
 // the zkey encoding.  The header points: alpha1 = alphaTauG1[0], beta1 = betaTauG1[0], beta2 =
-// betaG2, gamma2 = delta2 = G2, delta1 = G1.  Section 10 is the empty contribution list with a
-// zero csHash (the prover ignores it; snarkjs' circuit hash is not restated).
+// betaG2, gamma2 = delta2 = G2, delta1 = G1.  Section 10 is the empty contribution list with the
+// circuit hash (csHash, mpc.cpp / oracle/mpc.py: Blake2b-512 over the key's points and the ptau's
+// tauG1 powers), which `zkey verify` recomputes from the r1cs and ptau.
 // ptau / r1cs layouts: oracle/binfile.py write_ptau / write_r1cs (recalled, unpinned offline).
 #include <algorithm>
 #include <cstring>
@@ -24,6 +25,7 @@
 #include "curve.hpp"
 #include "hip_check.hpp"
 #include "host_ec.hpp"
+#include "mpc.hpp"
 #include "prover.hpp"
 #include "qap.hpp"
 
@@ -248,7 +250,7 @@ std::vector<uint8_t> zkey_new(int device, const uint8_t* r1cs, size_t r1cs_len, 
   while ((uint64_t(1) << k) < (uint64_t)n_cons + n_pub + 1) ++k;
   const uint32_t n = 1u << k;
   BinFile pb = parse_binfile(ptau, ptau_len, "ptau", 1);
-  for (int id : {1, 4, 5, 6, 12, 13, 14, 15})
+  for (int id : {1, 2, 4, 5, 6, 12, 13, 14, 15})
     if (!pb.sec[id].ptr) throw ZkpError(ZKP_ERR_FORMAT, "ptau: missing section " + std::to_string(id));
   uint32_t pn8, power;
   std::memcpy(&pn8, pb.sec[1].ptr, 4);
@@ -406,6 +408,9 @@ std::vector<uint8_t> zkey_new(int device, const uint8_t* r1cs, size_t r1cs_len, 
     put(out, (uint64_t)s.second.size());
     put_bytes(out, s.second.data(), s.second.size());
   }
+  // section 10 (the last, 68 bytes): the circuit hash over the new key's points and the ptau's
+  // tauG1 powers, as `snarkjs zkey new` writes it (mpc.cpp; `zkey verify` compares it)
+  mpc_cs_hash_new(out.data(), out.size(), pb.sec[2].ptr, (size_t)(pb.sec[2].len / 64), out.data() + out.size() - 68);
   return out;
 }
 

@@ -9,15 +9,17 @@
  *   node cli.js zkey export soliditycalldata <public.json> <proof.json>
  * and snarkjs' setup step (reference dizkus-scripts/3_gen_chunk_zkey.sh:18, `groth16 setup`):
  *   node cli.js groth16 setup|zkey new <circuit.r1cs> <pot.ptau> <circuit_0000.zkey> [-e=...]
- * and the final beacon (3_gen_chunk_zkey.sh:36; no transcript record is appended):
+ * a contribution and the final beacon (3_gen_chunk_zkey.sh:27,36; the record is appended to section 10):
+ *   node cli.js zkey contribute <in.zkey> <out.zkey> -e=<entropy> [-n=name]
  *   node cli.js zkey beacon <in.zkey> <out.zkey> <beaconHashHex> <numIterationsExp> [-n=name]
  */
 const fs = require('fs');
-const { groth16, exportSolidityCallData, newZKey, beacon, release } = require('./groth16');
+const { groth16, exportSolidityCallData, newZKey, beacon, contribute, release } = require('./groth16');
 
 const USAGE = 'usage: cli.js groth16 prove <circuit.zkey> <witness.wtns> <proof.json> <public.json>\n' +
               '       cli.js zkey export soliditycalldata <public.json> <proof.json>\n' +
               '       cli.js groth16 setup|zkey new <circuit.r1cs> <pot.ptau> <circuit_0000.zkey>\n' +
+              '       cli.js zkey contribute <in.zkey> <out.zkey> -e=<entropy> [-n=name]\n' +
               '       cli.js zkey beacon <in.zkey> <out.zkey> <beaconHashHex> <numIterationsExp> [-n=name]\n';
 
 async function main(argv) {
@@ -33,6 +35,15 @@ async function main(argv) {
     return 0;
   }
   const named = argv.filter((a) => !/^(-n|--name)=/.test(a) && a !== '-v' && a !== '--verbose');
+  if (argv[0] === 'zkey' && argv[1] === 'contribute') {
+    const pos = argv.filter((a) => !a.startsWith('-'));
+    const ent = argv.find((a) => /^(-e|--entropy)=/.test(a));
+    const nameArg = argv.find((a) => /^(-n|--name)=/.test(a));
+    if (pos.length === 4 && ent) {
+      await contribute(pos[2], pos[3], nameArg ? nameArg.replace(/^[^=]*=/, '') : '', ent.replace(/^[^=]*=/, ''));
+      return 0;
+    }
+  }
   if (named.length === 6 && argv[0] === 'zkey' && argv[1] === 'beacon') {
     const nameArg = argv.find((a) => /^(-n|--name)=/.test(a));
     await beacon(named[2], named[3], nameArg ? nameArg.replace(/^[^=]*=/, '') : '', named[4], named[5]);

@@ -151,9 +151,9 @@ async function newZKey(r1csName, ptauName, zkeyName, logger, device) {
 
 /*
  * snarkjs' `zKey.beacon(zkeyNameOld, zkeyNameNew, name, beaconHashStr, numIterationsExp, logger)`
- * (reference dizkus-scripts/3_gen_chunk_zkey.sh:36): delta -> k delta, L/H -> k^-1, with k
- * derived from the beacon as snarkjs does, on the GPU.  The contribution record (section 10)
- * is not appended: `snarkjs zkey verify` will not list this contribution.
+ * (reference dizkus-scripts/3_gen_chunk_zkey.sh:36): delta -> k delta, L/H -> k^-1 on the GPU, with
+ * k and the contribution record (section 10: proof of knowledge, transcript, beacon parameters,
+ * name) derived from the beacon as snarkjs does (oracle/mpc.py restates it; parity unpinned).
  */
 async function beacon(zkeyNameOld, zkeyNameNew, name, beaconHashStr, numIterationsExp, logger, device) {
   const hex = String(beaconHashStr);
@@ -161,10 +161,26 @@ async function beacon(zkeyNameOld, zkeyNameNew, name, beaconHashStr, numIteratio
   if (bytes.length === 0) throw new Error('Invalid Beacon Hash. (It must be a valid hexadecimal sequence)');
   const e = Number(numIterationsExp);
   if (!Number.isInteger(e) || e < 10 || e > 63) throw new Error('Invalid numIterationsExp. (Must be between 10 and 63)');
-  const out = addon.zkeyBeacon(readInput(zkeyNameOld), bytes, e, device || 0);
+  const out = addon.zkeyBeacon(readInput(zkeyNameOld), bytes, e, device || 0, name ? String(name) : undefined);
   if (typeof zkeyNameNew === 'string') fs.writeFileSync(zkeyNameNew, out);
   else if (zkeyNameNew && typeof zkeyNameNew === 'object' && zkeyNameNew.type === 'mem') zkeyNameNew.data = out;
   if (logger && logger.info) logger.info(`zkey beacon ${name || ''}: ${out.length} bytes`);
+  return out;
+}
+
+/*
+ * snarkjs' `zKey.contribute(zkeyNameOld, zkeyNameNew, name, entropy, logger)` (reference
+ * dizkus-scripts/3_gen_chunk_zkey.sh:27, `zkey contribute -e=... -n=...`): the secret and the
+ * record drawn from ChaCha20 seeded with Blake2b(64 random bytes || entropy), the group arithmetic
+ * on the GPU.
+ */
+async function contribute(zkeyNameOld, zkeyNameNew, name, entropy, logger, device) {
+  if (!entropy) throw new Error('zkey contribute: entropy is required (-e=...)');
+  const out = addon.zkeyContribute(readInput(zkeyNameOld), String(entropy), name ? String(name) : undefined,
+                                   device || 0);
+  if (typeof zkeyNameNew === 'string') fs.writeFileSync(zkeyNameNew, out);
+  else if (zkeyNameNew && typeof zkeyNameNew === 'object' && zkeyNameNew.type === 'mem') zkeyNameNew.data = out;
+  if (logger && logger.info) logger.info(`zkey contribute ${name || ''}: ${out.length} bytes`);
   return out;
 }
 
@@ -178,9 +194,10 @@ function release() {
 module.exports = {
   groth16: { prove, proveBatch },
   proveBatch,
-  zKey: { exportSolidityCallData, newZKey, beacon },
+  zKey: { exportSolidityCallData, newZKey, beacon, contribute },
   newZKey,
   beacon,
+  contribute,
   prove,
   exportSolidityCallData,
   onRampArgs,

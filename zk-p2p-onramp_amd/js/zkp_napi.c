@@ -10,7 +10,8 @@
  *                                                    every proof attempted, per-proof errors)
  *   freeProver(handle)
  *   zkeyNew(r1csBuffer, ptauBuffer, device?)     -> Buffer (`snarkjs zkey new`, synchronous)
- *   zkeyBeacon(zkeyBuffer, beaconBuffer, numIterationsExp, device?) -> Buffer (`zkey beacon` math)
+ *   zkeyBeacon(zkeyBuffer, beaconBuffer, numIterationsExp, device?, name?) -> Buffer (`zkey beacon`)
+ *   zkeyContribute(zkeyBuffer, entropy, name?, device?) -> Buffer (`zkey contribute`)
  *   version()
  * prove()/proveBatch() run on the libuv threadpool (napi_async_work), so the JS main
  * thread is never blocked — the same async contract as snarkjs' Promise API.
@@ -116,11 +117,65 @@ static napi_value js_zkey_new(napi_env env, napi_callback_info info) {
   return buf;
 }
 
-/* zkeyBeacon(zkeyBuffer, beaconBuffer, numIterationsExp, device?) -> Buffer: the group
- * arithmetic of `snarkjs zkey beacon` (zkp_zkey_beacon), synchronous */
-static napi_value js_zkey_beacon(napi_env env, napi_callback_info info) {
+/* a JS string argument into buf (NULL when absent / undefined / not a string) */
+static const char* opt_string(napi_env env, napi_value v, char* buf, size_t cap) {
+  napi_valuetype t;
+  if (napi_typeof(env, v, &t) != napi_ok || t != napi_string) return NULL;
+  size_t n = 0;
+  if (napi_get_value_string_utf8(env, v, buf, cap, &n) != napi_ok) return NULL;
+  return buf;
+}
+
+static napi_value buffer_out(napi_env env, uint8_t* out, size_t out_len) {
+  napi_value buf;
+  void* dst = NULL;
+  napi_status ns = napi_create_buffer(env, out_len, &dst, &buf);
+  if (ns == napi_ok) memcpy(dst, out, out_len);
+  zkp_buffer_free(out);
+  if (ns != napi_ok) {
+    napi_throw_error(env, NULL, "N-API call failed: napi_create_buffer");
+    return NULL;
+  }
+  return buf;
+}
+
+/* zkeyContribute(zkeyBuffer, entropyString, nameString?, device?) -> Buffer: `snarkjs zkey
+ * contribute -e=... -n=...` (zkp_zkey_contribute_entropy: 64 bytes of /dev/urandom mixed with the
+ * entropy, the contribution record appended), synchronous */
+static napi_value js_zkey_contribute(napi_env env, napi_callback_info info) {
   size_t argc = 4;
   napi_value argv[4];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  bool b0 = false;
+  char ent[4096], name[256];
+  const char* e = NULL;
+  if (argc >= 2) {
+    napi_is_buffer(env, argv[0], &b0);
+    e = opt_string(env, argv[1], ent, sizeof ent);
+  }
+  if (!b0 || !e) {
+    napi_throw_type_error(env, NULL, "zkeyContribute(zkeyBuffer, entropyString, nameString?, device?)");
+    return NULL;
+  }
+  const char* nm = argc > 2 ? opt_string(env, argv[2], name, sizeof name) : NULL;
+  int device = 0;
+  if (argc > 3) napi_get_value_int32(env, argv[3], &device);
+  void* zkey;
+  size_t zkey_len;
+  NAPI_CALL(env, napi_get_buffer_info(env, argv[0], &zkey, &zkey_len));
+  uint8_t* out = NULL;
+  size_t out_len = 0;
+  zkp_status st = zkp_zkey_contribute_entropy(device, (const uint8_t*)zkey, zkey_len, NULL, e, nm, &out, &out_len);
+  if (st != ZKP_OK) return throw_status(env, st);
+  return buffer_out(env, out, out_len);
+}
+
+/* zkeyBeacon(zkeyBuffer, beaconBuffer, numIterationsExp, device?, nameString?) -> Buffer:
+ * `snarkjs zkey beacon` (zkp_zkey_beacon_named: GPU group arithmetic + the type-1 record),
+ * synchronous */
+static napi_value js_zkey_beacon(napi_env env, napi_callback_info info) {
+  size_t argc = 5;
+  napi_value argv[5];
   NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
   bool b0 = false, b1 = false;
   uint32_t e = 0;
@@ -140,19 +195,12 @@ static napi_value js_zkey_beacon(napi_env env, napi_callback_info info) {
   NAPI_CALL(env, napi_get_buffer_info(env, argv[1], &beacon, &beacon_len));
   uint8_t* out = NULL;
   size_t out_len = 0;
-  zkp_status st = zkp_zkey_beacon(device, (const uint8_t*)zkey, zkey_len, (const uint8_t*)beacon, beacon_len, e, &out,
-                                  &out_len);
+  char name[256];
+  const char* nm = argc > 4 ? opt_string(env, argv[4], name, sizeof name) : NULL;
+  zkp_status st = zkp_zkey_beacon_named(device, (const uint8_t*)zkey, zkey_len, (const uint8_t*)beacon, beacon_len, e,
+                                        nm, &out, &out_len);
   if (st != ZKP_OK) return throw_status(env, st);
-  napi_value buf;
-  void* dst = NULL;
-  napi_status ns = napi_create_buffer(env, out_len, &dst, &buf);
-  if (ns == napi_ok) memcpy(dst, out, out_len);
-  zkp_buffer_free(out);
-  if (ns != napi_ok) {
-    napi_throw_error(env, NULL, "N-API call failed: napi_create_buffer");
-    return NULL;
-  }
-  return buf;
+  return buffer_out(env, out, out_len);
 }
 
 static napi_value js_load(napi_env env, napi_callback_info info) {
@@ -546,6 +594,7 @@ static napi_value init(napi_env env, napi_value exports) {
       {"freeProver", NULL, js_free, NULL, NULL, NULL, napi_default, NULL},
       {"zkeyNew", NULL, js_zkey_new, NULL, NULL, NULL, napi_default, NULL},
       {"zkeyBeacon", NULL, js_zkey_beacon, NULL, NULL, NULL, napi_default, NULL},
+      {"zkeyContribute", NULL, js_zkey_contribute, NULL, NULL, NULL, napi_default, NULL},
   };
   napi_define_properties(env, exports, sizeof props / sizeof props[0], props);
   return exports;

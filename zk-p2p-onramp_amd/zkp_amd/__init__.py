@@ -129,10 +129,15 @@ def load_library(path: str = LIB_PATH):
                                           ctypes.POINTER(_Proof)]
         lib.zkp_quotient_part_staged.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.POINTER(P)]
         lib.zkp_prove_partial_ext_staged.argtypes = [P, ctypes.c_int, ctypes.POINTER(P), ctypes.c_char_p]
+        lib.zkp_zkey_beacon_named.argtypes = [ctypes.c_int, u8p, sz, u8p, sz, ctypes.c_uint32, ctypes.c_char_p,
+                                              ctypes.POINTER(u8p), ctypes.POINTER(sz)]
+        lib.zkp_zkey_contribute_entropy.argtypes = [ctypes.c_int, u8p, sz, u8p, ctypes.c_char_p, ctypes.c_char_p,
+                                                    ctypes.POINTER(u8p), ctypes.POINTER(sz)]
+        lib.zkp_blake2b512.argtypes = [u8p, sz, u8p]
         lib.zkp_prover_set_verify.argtypes = [P, ctypes.c_int]
         lib.zkp_proof_verify.argtypes = [u8p, sz, ctypes.POINTER(_Proof), ctypes.POINTER(ctypes.c_int)]
         lib.zkp_pairing.argtypes = [u8p, u8p, u8p]
-        for name in ("zkp_prover_set_verify", "zkp_proof_verify", "zkp_pairing", "zkp_prover_load_mem", "zkp_prover_load_file", "zkp_prover_info", "zkp_prove",
+        for name in ("zkp_zkey_beacon_named", "zkp_zkey_contribute_entropy", "zkp_blake2b512", "zkp_prover_set_verify", "zkp_proof_verify", "zkp_pairing", "zkp_prover_load_mem", "zkp_prover_load_file", "zkp_prover_info", "zkp_prove",
                      "zkp_prove_batch", "zkp_prove_batch_status", "zkp_prove_files", "zkp_proof_json", "zkp_public_json",
                      "zkp_prover_timings", "zkp_msm_g1", "zkp_msm_g2", "zkp_ntt_fr", "zkp_quotient",
                      "zkp_witness_stage", "zkp_prove_staged", "zkp_prover_instrument", "zkp_prover_kernel_stats",
@@ -517,20 +522,48 @@ def beacon_secret(beacon: bytes, num_iterations_exp: int) -> int:
     return int.from_bytes(bytes(k), "little")
 
 
-def zkey_beacon(zkey: bytes, beacon: bytes, num_iterations_exp: int, device: int = 0) -> bytes:
-    """`snarkjs zkey beacon`'s group arithmetic on the GPU: delta -> k*delta with k the beacon's
-    secret (zkp_zkey_beacon; section 10 unchanged)."""
+def zkey_beacon(zkey: bytes, beacon: bytes, num_iterations_exp: int, device: int = 0, name=None) -> bytes:
+    """`snarkjs zkey beacon <in> <out> <hex> <e> [-n=name]` (zkp_zkey_beacon_named): delta -> k*delta
+    with k the beacon's secret on the GPU, the type-1 contribution record appended to section 10."""
     lib = load_library()
     zp, zk = _buf(zkey)
     bp, bk = _buf(bytes(beacon) or b"\0")
     out = ctypes.POINTER(ctypes.c_uint8)()
     n = ctypes.c_size_t()
-    _check(lib.zkp_zkey_beacon(device, zp, len(zkey), bp, len(beacon), num_iterations_exp, ctypes.byref(out),
-                               ctypes.byref(n)))
+    _check(lib.zkp_zkey_beacon_named(device, zp, len(zkey), bp, len(beacon), num_iterations_exp,
+                                     name.encode() if name else None, ctypes.byref(out), ctypes.byref(n)))
     try:
         return _copy_out(out, n.value)
     finally:
         lib.zkp_buffer_free(out)
+
+
+def zkey_contribute_entropy(zkey: bytes, entropy: str, rand64: bytes = None, name=None, device: int = 0) -> bytes:
+    """`snarkjs zkey contribute <in> <out> -e=<entropy> [-n=name]` (zkp_zkey_contribute_entropy):
+    rand64 = the 64 random bytes mixed with the entropy (None: /dev/urandom; tests pass fixed bytes)."""
+    lib = load_library()
+    zp, zk = _buf(zkey)
+    rp = None
+    if rand64 is not None:
+        if len(rand64) != 64:
+            raise ValueError("rand64 must be 64 bytes")
+        rp, rk = _buf(bytes(rand64))
+    out = ctypes.POINTER(ctypes.c_uint8)()
+    n = ctypes.c_size_t()
+    _check(lib.zkp_zkey_contribute_entropy(device, zp, len(zkey), rp, entropy.encode(), name.encode() if name else None,
+                                           ctypes.byref(out), ctypes.byref(n)))
+    try:
+        return _copy_out(out, n.value)
+    finally:
+        lib.zkp_buffer_free(out)
+
+
+def blake2b512(data: bytes) -> bytes:
+    """Host-only Blake2b-512 of the C++ MPC code (zkp_blake2b512)."""
+    dp, dk = _buf(bytes(data) or b"\0")
+    out = (ctypes.c_uint8 * 64)()
+    _check(load_library().zkp_blake2b512(dp, len(data), ctypes.cast(out, ctypes.POINTER(ctypes.c_uint8))))
+    return bytes(out)
 
 
 def zkey_new(r1cs: bytes, ptau: bytes, device: int = 0) -> bytes:
