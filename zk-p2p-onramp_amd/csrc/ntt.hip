@@ -1,6 +1,7 @@
 // Fr NTT engine (see ntt.hpp for the algorithm).
 #include "ntt.hpp"
 
+#include <cstdlib>
 #include <stdexcept>
 
 #include "field.hpp"
@@ -70,7 +71,8 @@ __device__ __forceinline__ void put_root(uint32_t* __restrict__ ltw, int j, cons
   for (int l = 0; l < NL; ++l) ltw[l * MAX_TW + j] = x.v[l];
 #endif
 }
-__device__ __forceinline__ void stage_roots(uint32_t* __restrict__ ltw, const uint32_t* __restrict__ loc, int b) {
+// the stage roots of a b-bit pass staged in LDS from the w_1024 table, in every workgroup
+__device__ __forceinline__ void stage_roots_loc(uint32_t* __restrict__ ltw, const uint32_t* __restrict__ loc, int b) {
   const int TW = 1 << (b - 1);
   for (int j = threadIdx.x; j < TW; j += TPB) {
     const Fr x = load_fe<FrCfg>(loc + (size_t)(j << (LOC_LOG - b)) * 8);  // canonical Montgomery form
@@ -88,6 +90,39 @@ __device__ __forceinline__ void stage_roots(uint32_t* __restrict__ ltw, const ui
 #endif
   }
 }
+
+// Shoup builds: the roots precomputed once per (direction, b) in their LDS layout (k_root_table),
+// so staging is a copy instead of two products per root per workgroup (~4 % of a pass's
+// multiplies); rtab == nullptr (ZKP_NTT_RTAB=0) stages them from the w_1024 table
+__device__ __forceinline__ void stage_roots(uint32_t* __restrict__ ltw, const uint32_t* __restrict__ rtab,
+                                            const uint32_t* __restrict__ loc, int b) {
+  if (!ZKP_NTT_SHOUP || !rtab) {
+    stage_roots_loc(ltw, loc, b);
+    return;
+  }
+  const uint4* s = reinterpret_cast<const uint4*>(rtab);
+  uint4* d = reinterpret_cast<uint4*>(ltw);
+  for (int k = threadIdx.x; k < RW * MAX_TW / 4; k += TPB) d[k] = s[k];
+}
+
+#if ZKP_NTT_SHOUP
+// rtab in the LDS layout of stage_roots: ltw[l * MAX_TW + j], j < 2^(b-1) (the rest zero)
+__global__ __launch_bounds__(TPB) void k_root_table(uint32_t* __restrict__ rtab, const uint32_t* __restrict__ loc, int b) {
+  const int j = blockIdx.x * TPB + threadIdx.x;
+  if (j >= MAX_TW) return;
+  Fr w = fe_zero<FrCfg>(), wq = fe_zero<FrCfg>();
+  if (j < (1 << (b - 1))) {
+    const Fr x = load_fe<FrCfg>(loc + (size_t)(j << (LOC_LOG - b)) * 8);  // canonical Montgomery form
+    w = from_mont(x);
+    wq = shoup_quot(x);
+  }
+#pragma unroll
+  for (int l = 0; l < NL; ++l) {
+    rtab[l * MAX_TW + j] = w.v[l];
+    rtab[(NL + l) * MAX_TW + j] = wq.v[l];
+  }
+}
+#endif
 
 // LDS data-tile swizzle: element e lives at word e ^ S(e), S(e) = (h ^ 2h ^ 8h) mod 32, h = e >> 5
 // (an XOR of bits 5.. into the bank bits 0..4).  ds_read_b32 / ds_write_b32 banks are word mod 32 per
@@ -251,7 +286,8 @@ __device__ __forceinline__ int brev_src(const Tile& T, int e) {
 // MODE 0: DIF pass (DFT, then inter-pass twiddle), 1: DIT pass (twiddle, then DFT),
 // 2: the fused innermost pair of coset_extend (lm == b): inverse-root DFT, coset key
 //    (table by digit-reversed position), forward-root DFT on one LDS-resident tile.
-// tw: w_(2^lm)^(col*row) by position in block (null when n2 == 1).
+// tw: w_(2^lm)^(col*row) by position in block (null when n2 == 1).  rootsA / rootsB: the stage
+// roots (Shoup builds: the k_root_table of this b; else the w_1024 table), B for MODE 2's forward DFT.
 #if ZKP_NTT_WPE
 #define NTT_WPE_ATTR __attribute__((amdgpu_waves_per_eu(ZKP_NTT_WPE)))
 #else
@@ -259,13 +295,14 @@ __device__ __forceinline__ int brev_src(const Tile& T, int e) {
 #endif
 template <int MODE>
 __global__ __launch_bounds__(TPB) NTT_WPE_ATTR void k_ntt(uint32_t* __restrict__ data, Tile T, const uint32_t* __restrict__ tw,
+                                             const uint32_t* __restrict__ rootsA, const uint32_t* __restrict__ rootsB,
                                              const uint32_t* __restrict__ locA, const uint32_t* __restrict__ locB,
                                              const uint32_t* __restrict__ coset) {
   __shared__ uint32_t lds[NL << LOG_TILE];  // SoA: lds[limb * E + element]
-  __shared__ uint32_t ltw[RW * MAX_TW];
+  __shared__ __attribute__((aligned(16))) uint32_t ltw[RW * MAX_TW];
   const int E = 1 << (T.b + T.lc + T.lbt);
   const uint32_t tile = blockIdx.x;
-  stage_roots(ltw, locA, T.b);
+  stage_roots(ltw, rootsA, locA, T.b);
   for (int e = threadIdx.x; e < E; e += TPB) {
     size_t g;
     uint32_t pos;
@@ -293,7 +330,7 @@ __global__ __launch_bounds__(TPB) NTT_WPE_ATTR void k_ntt(uint32_t* __restrict__
       v[idx] = mul(x, load_fe<FrCfg>(coset + g * 8));
     }
     __syncthreads();
-    stage_roots(ltw, locB, T.b);  // the forward roots replace the inverse ones (no reader until the next barrier)
+    stage_roots(ltw, rootsB, locB, T.b);  // the forward roots replace the inverse ones (no reader until the next barrier)
     idx = 0;
     for (int e = threadIdx.x; e < E; e += TPB, ++idx) {
 #pragma unroll
@@ -475,6 +512,21 @@ NttEngine::NttEngine(int log_n, hipStream_t stream) : log_n_(log_n), stream_(str
   coset_lo_ = upload_powers(g, nlo, 1, ninv, stream_);
   coset_hi_ = upload_powers(g, nhi, nlo, one, stream_);
   ninv_ = upload_powers(one, 1, 1, ninv, stream_);
+#if ZKP_NTT_SHOUP
+  // stage-root tables per (direction, pass bits) in the kernels' LDS layout (k_root_table);
+  // ZKP_NTT_RTAB=0 stages them from the w_1024 table in every workgroup instead (A/B knob)
+  {
+    const char* e = std::getenv("ZKP_NTT_RTAB");
+    use_rtab_ = !(e && std::atoi(e) == 0);
+  }
+  for (int dir = 0; dir < 2; ++dir)
+    for (int b : bits_)
+      if (!rtab_[dir][b]) {
+        HIPX(hipMalloc(&rtab_[dir][b], (size_t)RW * MAX_TW * 4));
+        hipLaunchKernelGGL(k_root_table, dim3((MAX_TW + TPB - 1) / TPB), dim3(TPB), 0, stream_, rtab_[dir][b],
+                           loc_[dir], b);
+      }
+#endif
   // per-pass twiddle tables (one multiply per element instead of lo*hi per element) and
   // the coset key by digit-reversed position: ~3 n x 32 B of HBM
   for (int dir = 0; dir < 2; ++dir) {
@@ -507,6 +559,9 @@ NttEngine::~NttEngine() {
   for (auto& v : tw_pass_)
     for (uint32_t* p : v)
       if (p) (void)hipFree(p);
+  for (auto& d : rtab_)
+    for (uint32_t* p : d)
+      if (p) (void)hipFree(p);
 }
 
 // mode 0: DIF pass p, 1: DIT (transposed) pass p, 2: fused innermost pass (inverse then forward)
@@ -515,15 +570,19 @@ void NttEngine::launch_pass(uint32_t* data, int mode, int p, bool inv) {
   const Tile T = make_tile(k, lms_[p], bits_[p]);
   const size_t tiles = (size_t(1) << k) >> (T.b + T.lc + T.lbt);
   const int d = inv ? 1 : 0;
+  const bool rt = use_rtab_;
+  const uint32_t *ra = rt ? rtab_[d][T.b] : nullptr, *rinv = rt ? rtab_[1][T.b] : nullptr,
+                 *rfwd = rt ? rtab_[0][T.b] : nullptr;
+  const uint32_t* none = nullptr;
   if (mode == 0)
-    hipLaunchKernelGGL(k_ntt<0>, dim3((unsigned)tiles), dim3(TPB), 0, stream_, data, T, tw_pass_[d][p], loc_[d],
-                       (const uint32_t*)nullptr, (const uint32_t*)nullptr);
+    hipLaunchKernelGGL(k_ntt<0>, dim3((unsigned)tiles), dim3(TPB), 0, stream_, data, T, tw_pass_[d][p], ra, none,
+                       loc_[d], none, none);
   else if (mode == 1)
-    hipLaunchKernelGGL(k_ntt<1>, dim3((unsigned)tiles), dim3(TPB), 0, stream_, data, T, tw_pass_[d][p], loc_[d],
-                       (const uint32_t*)nullptr, (const uint32_t*)nullptr);
+    hipLaunchKernelGGL(k_ntt<1>, dim3((unsigned)tiles), dim3(TPB), 0, stream_, data, T, tw_pass_[d][p], ra, none,
+                       loc_[d], none, none);
   else
-    hipLaunchKernelGGL(k_ntt<2>, dim3((unsigned)tiles), dim3(TPB), 0, stream_, data, T, (const uint32_t*)nullptr,
-                       loc_[1], loc_[0], coset_pos_);
+    hipLaunchKernelGGL(k_ntt<2>, dim3((unsigned)tiles), dim3(TPB), 0, stream_, data, T, none, rinv, rfwd, loc_[1],
+                       loc_[0], coset_pos_);
 }
 
 void NttEngine::dif_passes(uint32_t* data, bool inv, int first, int last) {
