@@ -116,11 +116,14 @@ def test_msm_g1_dense_counting_sort(monkeypatch):
         assert zkp_amd.msm_g1(pb, sb, window_bits=c, table_depth=d) == groth16.msm_g1(p, [x % R for x in s]), (c, d)
 
 
-@pytest.mark.parametrize("c", [17, 18, 19, 21, 22])
-def test_msm_dense_window_bits(monkeypatch, c):
+@pytest.mark.parametrize("balanced", [0, 1], ids=["uniform", "balanced"])
+@pytest.mark.parametrize("c", [17, 18, 19, 20, 21, 22])
+def test_msm_dense_window_bits(monkeypatch, c, balanced):
     # the hand-written sort's bin / sub-bin / bucket bit splits of every window width around the
     # prover's choices (c = 18: 6 + 6 + 5 bits, 19: 7 + 6 + 5, 21: 8 + 7 + 5 ...), 2^15 uniform
-    # scalars over 64 bases: dense plan == compacted plan == the oracle's sum
+    # scalars over 64 bases: dense plan == compacted plan == the oracle's sum; with balanced window
+    # widths (ZKP_MSM_BALANCED=1: windows of c and c - 1 bits, the H plan's ZKP_H_BALANCED) too
+    monkeypatch.setenv("ZKP_MSM_BALANCED", str(balanced))
     rng = circuit.SplitMix64(46, 1)
     n = 1 << 15
     g = bn254.FixedBase(bn254.G1_GEN)

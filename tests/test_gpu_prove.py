@@ -39,7 +39,11 @@ def test_prove_bit_exact(golden_dir, name):
 # every variant must give the same golden proof
 KNOBS = [{"ZKP_H_DENSE": "0"}, {"ZKP_H_SORT": "rocprim"}, {"ZKP_TASK_ORDER": "bucket"}, {"ZKP_SEG_M": "16", "ZKP_SUB_L": "4"}, {"ZKP_SEG_M": "2", "ZKP_SUB_L": "16"},
          {"ZKP_SCHED": "4"}, {"ZKP_SCHED": "5"}, {"ZKP_G2_FINISH_GATE": "1"}, {"ZKP_G2_FINISH_GATE": "2"},
-         {"ZKP_SUBSET_TREE": "0"}, {"ZKP_TREE_FIRST_MAX": "0"}]
+         {"ZKP_SUBSET_TREE": "0"}, {"ZKP_TREE_FIRST_MAX": "0"},
+         # round 3: balanced H-plan windows, the witness plan on rocprim / the low-priority stream,
+         # the tiled pass C for the H plan, the NTT roots staged per workgroup
+         {"ZKP_H_BALANCED": "1"}, {"ZKP_H_BALANCED": "0"}, {"ZKP_W_SORT": "rocprim"}, {"ZKP_WPLAN_HI": "0"},
+         {"ZKP_HS_TILED_C": "1"}, {"ZKP_NTT_RTAB": "0"}]
 
 
 @pytest.mark.parametrize("knobs", KNOBS, ids=lambda k: ",".join("%s=%s" % kv for kv in k.items()))

@@ -1,6 +1,6 @@
 // CPU replay of the MSM pipeline (msm_kernels.hpp per-thread bodies, same
 // parameters as MsmEngine) for debugging without a GPU.
-// usage: msm_emu <g1|g2> <file: points(zkey layout)|scalars> <n> [c] [depth]   -> prints affine result (hex words)
+// usage: msm_emu <g1|g2> <file: points(zkey layout)|scalars> <n> [c] [depth] [balanced 0|1]   -> prints affine result (hex words)
 #include <algorithm>
 #include <cstdio>
 #include <numeric>
@@ -11,7 +11,7 @@
 using namespace zkp;
 
 template <class F, class HF>
-static host::Jac<HF> run(std::vector<uint32_t>& pts, std::vector<uint32_t>& sc, uint32_t n, int c_ovr, int d_ovr) {
+static host::Jac<HF> run(std::vector<uint32_t>& pts, std::vector<uint32_t>& sc, uint32_t n, int c_ovr, int d_ovr, bool bal) {
   constexpr int FW = FWords<F>::W;
   // convert points to device layout
   for (size_t i = 0; i < pts.size() / 8; ++i) {
@@ -19,13 +19,13 @@ static host::Jac<HF> run(std::vector<uint32_t>& pts, std::vector<uint32_t>& sc, 
     x = mul(x, fe_const<FqCfg>(Conv::FQ_ZKEY_TO_DEV));
     store_fe(&pts[i * 8], x);
   }
-  MsmParams prm = MsmParams::make(std::max<uint32_t>(n, 1), c_ovr, d_ovr);
+  MsmParams prm = MsmParams::make(std::max<uint32_t>(n, 1), c_ovr, d_ovr, bal);
   const uint32_t W = prm.windows, T = prm.depth, G = prm.groups, half = 1u << (prm.c - 1), nb = G * half;
   // base table rows 1..T-1 (as MsmBases::extend)
   std::vector<uint32_t> table((size_t)T * n * 2 * FW);
   std::copy(pts.begin(), pts.begin() + (size_t)n * 2 * FW, table.begin());
   for (uint32_t t = 1; t < T; ++t)
-    for (uint32_t i = 0; i < n; ++i) msmk::extend_row<F>(i, table.data(), n, prm.c, (int)t);
+    for (uint32_t i = 0; i < n; ++i) msmk::extend_row<F>(i, table.data(), n, (int)t - 1 < prm.nb1 ? prm.c : prm.c - 1, (int)t);
   // compacted digit emission (window-major, point order) as k_digit_count/k_digit_write
   std::vector<std::vector<std::pair<uint32_t, uint32_t>>> per(W);
   for (uint32_t i = 0; i < n; ++i) {
@@ -33,7 +33,7 @@ static host::Jac<HF> run(std::vector<uint32_t>& pts, std::vector<uint32_t>& sc, 
     msmk::load_scalar(sc.data(), i, s);
     uint32_t carry = 0, key, val;
     for (uint32_t w = 0; w < W; ++w)
-      if (msmk::digit_entry(s, (int)w, prm.c, (int)T, n, i, carry, key, val)) per[w].push_back({key, val});
+      if (msmk::digit_entry(s, (int)w, prm.c, prm.nb1, (int)T, n, i, carry, key, val)) per[w].push_back({key, val});
   }
   std::vector<uint32_t> ks, vs;
   for (auto& v : per)
@@ -108,17 +108,18 @@ int main(int argc, char** argv) {
   FILE* f = fopen(argv[2], "rb");
   uint32_t n = atoi(argv[3]);
   const int c_ovr = argc > 4 ? atoi(argv[4]) : 0, d_ovr = argc > 5 ? atoi(argv[5]) : 0;
+  const bool bal = argc > 6 && atoi(argv[6]) == 1;  // balanced window widths
   size_t pw = g2 ? 32 : 16;
   std::vector<uint32_t> pts(n * pw), sc(n * 8 + 8);
   if (fread(pts.data(), 4, pts.size(), f) != pts.size()) return 1;
   if (fread(sc.data(), 4, n * 8, f) != n * 8) return 1;
   if (!g2) {
-    auto a = host::jac_to_aff(run<Fq, host::Fq>(pts, sc, n, c_ovr, d_ovr));
+    auto a = host::jac_to_aff(run<Fq, host::Fq>(pts, sc, n, c_ovr, d_ovr, bal));
     if (a.inf) { printf("inf\n"); return 0; }
     auto x = a.x.to_std(), y = a.y.to_std();
     printf("%s %s\n", host::u256_to_dec(x).c_str(), host::u256_to_dec(y).c_str());
   } else {
-    auto a = host::jac_to_aff(run<Fq2, host::Fq2>(pts, sc, n, c_ovr, d_ovr));
+    auto a = host::jac_to_aff(run<Fq2, host::Fq2>(pts, sc, n, c_ovr, d_ovr, bal));
     if (a.inf) { printf("inf\n"); return 0; }
     printf("%s %s %s %s\n", host::u256_to_dec(a.x.c0.to_std()).c_str(), host::u256_to_dec(a.x.c1.to_std()).c_str(),
            host::u256_to_dec(a.y.c0.to_std()).c_str(), host::u256_to_dec(a.y.c1.to_std()).c_str());

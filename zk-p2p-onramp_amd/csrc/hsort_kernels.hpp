@@ -199,8 +199,8 @@ __global__ __launch_bounds__(SC_TPB) void k_lvl_apply(const uint32_t* __restrict
 // ---------------------------------------------------------------- pass A: digits -> bins
 // a workgroup takes K * HS_TPB scalars (K * HS_TPB * W <= HS_STAGE entries), K per thread
 template <int K>
-__global__ __launch_bounds__(HS_TPB) void k_hs_count1(const uint32_t* __restrict__ scalars, uint32_t n, int c, int W,
-                                                      int T, int sh1, uint32_t nbins, uint32_t* __restrict__ hist) {
+__global__ __launch_bounds__(HS_TPB) void k_hs_count1(const uint32_t* __restrict__ scalars, uint32_t n, int c, int nb1,
+                                                      int W, int T, int sh1, uint32_t nbins, uint32_t* __restrict__ hist) {
   __shared__ uint32_t h[1 << HS_MAX_B1];
   for (uint32_t b = threadIdx.x; b < nbins; b += HS_TPB) h[b] = 0;
   __syncthreads();
@@ -213,7 +213,7 @@ __global__ __launch_bounds__(HS_TPB) void k_hs_count1(const uint32_t* __restrict
     uint32_t carry = 0;
     for (int w = 0; w < W; ++w) {
       uint32_t key, val;
-      if (msmk::digit_entry(s, w, c, T, n, i, carry, key, val)) atomicAdd(&h[key >> sh1], 1u);
+      if (msmk::digit_entry(s, w, c, nb1, T, n, i, carry, key, val)) atomicAdd(&h[key >> sh1], 1u);
     }
   }
   __syncthreads();
@@ -254,7 +254,7 @@ __global__ __launch_bounds__(512) void k_hs_binbase(const uint32_t* __restrict__
 // atomics), then the stage written out linearly: consecutive lanes, consecutive addresses of a run
 template <int K>
 __global__ __launch_bounds__(HS_TPB) void k_hs_scatter1(const uint32_t* __restrict__ scalars, uint32_t n, int c,
-                                                        int W, int T, int sh1, uint32_t nbins,
+                                                        int nb1, int W, int T, int sh1, uint32_t nbins,
                                                         const uint32_t* __restrict__ blkoff,
                                                         const uint32_t* __restrict__ binbase,
                                                         uint2* __restrict__ ent) {
@@ -283,7 +283,7 @@ __global__ __launch_bounds__(HS_TPB) void k_hs_scatter1(const uint32_t* __restri
       e[q][w] = make_uint2(NONE, 0u);
       if (w < W) {
         uint32_t key, val;
-        if (msmk::digit_entry(s, w, c, T, n, i, carry, key, val) && act) {
+        if (msmk::digit_entry(s, w, c, nb1, T, n, i, carry, key, val) && act) {
           e[q][w] = make_uint2(key, val);
           atomicAdd(&cnt[key >> sh1], 1u);
         }

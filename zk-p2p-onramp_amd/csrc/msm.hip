@@ -30,13 +30,13 @@ __device__ __forceinline__ uint32_t lane_rank(uint64_t m) {  // set bits of m be
 // row t of the base table from row t-1: 2^c * P, affine.  One launch per row keeps
 // every launch short (~T-1 launches of n threads at zkey load).
 template <class F>
-__global__ __launch_bounds__(TPB) void k_extend_row(uint32_t* __restrict__ table, uint32_t n, int c, int t) {
-  msmk::extend_row<F>(blockIdx.x * TPB + threadIdx.x, table, n, c, t);
+__global__ __launch_bounds__(TPB) void k_extend_row(uint32_t* __restrict__ table, uint32_t n, int dbl, int t) {
+  msmk::extend_row<F>(blockIdx.x * TPB + threadIdx.x, table, n, dbl, t);
 }
 
 // pass 1 of the compacted digit emission: nonzero digits per (window, block)
-__global__ __launch_bounds__(TPB) void k_digit_count(const uint32_t* __restrict__ scalars, uint32_t n, int c, int W,
-                                                     uint32_t* __restrict__ bcnt) {
+__global__ __launch_bounds__(TPB) void k_digit_count(const uint32_t* __restrict__ scalars, uint32_t n, int c, int nb1,
+                                                     int W, uint32_t* __restrict__ bcnt) {
   __shared__ uint32_t cnt[MAX_WINDOWS];
   for (uint32_t w = threadIdx.x; w < (uint32_t)W; w += TPB) cnt[w] = 0;
   __syncthreads();
@@ -47,7 +47,7 @@ __global__ __launch_bounds__(TPB) void k_digit_count(const uint32_t* __restrict_
   uint32_t carry = 0;
   bool neg;
   for (int w = 0; w < W; ++w) {
-    const uint32_t mag = msmk::digit_mag(s, w, c, carry, neg);
+    const uint32_t mag = msmk::digit_mag(s, w, c, nb1, carry, neg);
     const uint64_t m = __ballot(active && mag != 0);
     if ((threadIdx.x & 63) == 0) atomicAdd(&cnt[w], (uint32_t)__popcll(m));
   }
@@ -58,8 +58,8 @@ __global__ __launch_bounds__(TPB) void k_digit_count(const uint32_t* __restrict_
 // pass 2: write (key, base | sign) of every nonzero digit at
 //   boff[window][block] + (entries of earlier waves of the block) + (earlier lanes of the wave)
 // -> window-major, point order within a window (deterministic)
-__global__ __launch_bounds__(TPB) void k_digit_write(const uint32_t* __restrict__ scalars, uint32_t n, int c, int W,
-                                                     int T, const uint32_t* __restrict__ boff,
+__global__ __launch_bounds__(TPB) void k_digit_write(const uint32_t* __restrict__ scalars, uint32_t n, int c, int nb1,
+                                                     int W, int T, const uint32_t* __restrict__ boff,
                                                      uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
   __shared__ uint32_t wcnt[MAX_WINDOWS][WAVES];
   const uint32_t i = blockIdx.x * TPB + threadIdx.x;
@@ -70,7 +70,7 @@ __global__ __launch_bounds__(TPB) void k_digit_write(const uint32_t* __restrict_
   uint32_t carry = 0;
   bool neg;
   for (int w = 0; w < W; ++w) {
-    const uint32_t mag = msmk::digit_mag(s, w, c, carry, neg);
+    const uint32_t mag = msmk::digit_mag(s, w, c, nb1, carry, neg);
     const uint64_t m = __ballot(active && mag != 0);
     if ((threadIdx.x & 63) == 0) wcnt[w][wave] = (uint32_t)__popcll(m);
   }
@@ -78,7 +78,7 @@ __global__ __launch_bounds__(TPB) void k_digit_write(const uint32_t* __restrict_
   carry = 0;
   for (int w = 0; w < W; ++w) {
     uint32_t key, val;
-    const bool valid = msmk::digit_entry(s, w, c, T, n, i, carry, key, val) && active;
+    const bool valid = msmk::digit_entry(s, w, c, nb1, T, n, i, carry, key, val) && active;
     const uint64_t m = __ballot(valid);
     if (valid) {
       uint32_t base = boff[(size_t)w * gridDim.x + blockIdx.x];
@@ -94,7 +94,7 @@ __global__ __launch_bounds__(TPB) void k_digit_write(const uint32_t* __restrict_
 // (window, point), a zero digit keyed `sentinel` (= the bucket count, sorted past every
 // bucket) -- no counting pass, no scan, no host round trip for the entry count
 __global__ __launch_bounds__(TPB) void k_digit_write_dense(const uint32_t* __restrict__ scalars, uint32_t n, int c,
-                                                           int W, int T, uint32_t sentinel,
+                                                           int nb1, int W, int T, uint32_t sentinel,
                                                            uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
   const uint32_t i = blockIdx.x * TPB + threadIdx.x;
   if (i >= n) return;
@@ -103,7 +103,7 @@ __global__ __launch_bounds__(TPB) void k_digit_write_dense(const uint32_t* __res
   uint32_t carry = 0;
   for (int w = 0; w < W; ++w) {
     uint32_t key, val;
-    const bool valid = msmk::digit_entry(s, w, c, T, n, i, carry, key, val);
+    const bool valid = msmk::digit_entry(s, w, c, nb1, T, n, i, carry, key, val);
     keys[(size_t)w * n + i] = valid ? key : sentinel;
     vals[(size_t)w * n + i] = val;
   }
@@ -280,8 +280,8 @@ __device__ __forceinline__ uint32_t lds_claim(uint32_t* h, uint32_t b, bool vali
   return valid ? atomicAdd(&h[b], 1u) : 0u;
 }
 
-__global__ __launch_bounds__(TPB) void k_bin_hist(const uint32_t* __restrict__ scalars, uint32_t n, int c, int W,
-                                                  int T, int fb, uint32_t nbins, uint32_t* __restrict__ hist) {
+__global__ __launch_bounds__(TPB) void k_bin_hist(const uint32_t* __restrict__ scalars, uint32_t n, int c, int nb1,
+                                                  int W, int T, int fb, uint32_t nbins, uint32_t* __restrict__ hist) {
   __shared__ uint32_t h[1 << MAX_COARSE_BITS];
   for (uint32_t b = threadIdx.x; b < nbins; b += TPB) h[b] = 0;
   __syncthreads();
@@ -293,7 +293,7 @@ __global__ __launch_bounds__(TPB) void k_bin_hist(const uint32_t* __restrict__ s
     uint32_t carry = 0;
     for (int w = 0; w < W; ++w) {
       uint32_t key, val;
-      const bool valid = msmk::digit_entry(s, w, c, T, n, i, carry, key, val) && active;
+      const bool valid = msmk::digit_entry(s, w, c, nb1, T, n, i, carry, key, val) && active;
       lds_claim(h, key >> fb, valid);
     }
   }
@@ -301,8 +301,8 @@ __global__ __launch_bounds__(TPB) void k_bin_hist(const uint32_t* __restrict__ s
   for (uint32_t b = threadIdx.x; b < nbins; b += TPB) hist[(size_t)b * gridDim.x + blockIdx.x] = h[b];
 }
 
-__global__ __launch_bounds__(TPB) void k_bin_scatter(const uint32_t* __restrict__ scalars, uint32_t n, int c, int W,
-                                                     int T, int fb, uint32_t nbins, const uint32_t* __restrict__ hoff,
+__global__ __launch_bounds__(TPB) void k_bin_scatter(const uint32_t* __restrict__ scalars, uint32_t n, int c, int nb1,
+                                                     int W, int T, int fb, uint32_t nbins, const uint32_t* __restrict__ hoff,
                                                      uint32_t* __restrict__ fine, uint32_t* __restrict__ vals) {
   __shared__ uint32_t cur[1 << MAX_COARSE_BITS];
   for (uint32_t b = threadIdx.x; b < nbins; b += TPB) cur[b] = hoff[(size_t)b * gridDim.x + blockIdx.x];
@@ -316,7 +316,7 @@ __global__ __launch_bounds__(TPB) void k_bin_scatter(const uint32_t* __restrict_
     uint32_t carry = 0;
     for (int w = 0; w < W; ++w) {
       uint32_t key, val;
-      const bool valid = msmk::digit_entry(s, w, c, T, n, i, carry, key, val) && active;
+      const bool valid = msmk::digit_entry(s, w, c, nb1, T, n, i, carry, key, val) && active;
       const uint32_t pos = lds_claim(cur, key >> fb, valid);
       if (valid) {
         fine[pos] = key & fmask;
@@ -493,7 +493,8 @@ void run_finish(const MsmPlan& plan, uint32_t* part_a, uint32_t* part_b, uint32_
 
 // ------------------------------------------------------------------ MsmBases
 
-MsmBases::MsmBases(Curve curve, size_t n, int c, int depth) : curve_(curve), n_(n), c_(c), depth_(depth) {
+MsmBases::MsmBases(Curve curve, size_t n, int c, int depth, int nb1)
+    : curve_(curve), n_(n), c_(c), depth_(depth), nb1_(nb1) {
   if (depth < 1 || c < 2) throw std::runtime_error("MsmBases: bad parameters");
   if ((size_t)depth * std::max<size_t>(n, 1) >= (size_t(1) << 31))
     throw std::runtime_error("MsmBases: depth * n must stay below 2^31 (31-bit base indices)");
@@ -508,10 +509,11 @@ MsmBases::~MsmBases() {
 void MsmBases::extend(hipStream_t st) {
   if (n_ == 0) return;
   for (int t = 1; t < depth_; ++t) {
+    const int dbl = t - 1 < nb1_ ? c_ : c_ - 1;  // the width of window t - 1
     if (curve_ == Curve::G1)
-      hipLaunchKernelGGL(k_extend_row<Fq>, dim3(grid_for(n_)), dim3(TPB), 0, st, d_, (uint32_t)n_, c_, t);
+      hipLaunchKernelGGL(k_extend_row<Fq>, dim3(grid_for(n_)), dim3(TPB), 0, st, d_, (uint32_t)n_, dbl, t);
     else
-      hipLaunchKernelGGL(k_extend_row<Fq2>, dim3(grid_for(n_)), dim3(TPB), 0, st, d_, (uint32_t)n_, c_, t);
+      hipLaunchKernelGGL(k_extend_row<Fq2>, dim3(grid_for(n_)), dim3(TPB), 0, st, d_, (uint32_t)n_, dbl, t);
   }
   HIPX(hipGetLastError());
 }
@@ -677,14 +679,14 @@ void MsmPlan::build(const uint32_t* scalars, size_t n) {
       uint2* eb = static_cast<uint2*>(hs_ent_b_);
       // A: digits -> bins
       auto count1 = k == 4 ? k_hs_count1<4> : (k == 2 ? k_hs_count1<2> : k_hs_count1<1>);
-      hipLaunchKernelGGL(count1, dim3(nblk), dim3(HS_TPB), 0, st, scalars, (uint32_t)n, prm_.c, (int)W, prm_.depth,
-                         sh1, hs_nbins_, hs_hist_);
+      hipLaunchKernelGGL(count1, dim3(nblk), dim3(HS_TPB), 0, st, scalars, (uint32_t)n, prm_.c, prm_.nb1, (int)W,
+                         prm_.depth, sh1, hs_nbins_, hs_hist_);
       hipLaunchKernelGGL(k_hs_binscan, dim3(hs_nbins_), dim3(HS_TPB), 0, st, hs_hist_, nblk, hs_blkoff_, hs_bintot_);
       hipLaunchKernelGGL(k_hs_binbase, dim3(1), dim3(512), 0, st, hs_bintot_, hs_nbins_, hs_binbase_, hs_toff_);
       auto scatter1 = k == 4 ? k_hs_scatter1<4> : (k == 2 ? k_hs_scatter1<2> : k_hs_scatter1<1>);
       const size_t lds1 = (size_t)k * HS_TPB * W * 8 + (size_t)hs_nbins_ * 8;
-      hipLaunchKernelGGL(scatter1, dim3(nblk), dim3(HS_TPB), lds1, st, scalars, (uint32_t)n, prm_.c, (int)W, prm_.depth,
-                         sh1, hs_nbins_, hs_blkoff_, hs_binbase_, ea);
+      hipLaunchKernelGGL(scatter1, dim3(nblk), dim3(HS_TPB), lds1, st, scalars, (uint32_t)n, prm_.c, prm_.nb1, (int)W,
+                         prm_.depth, sh1, hs_nbins_, hs_blkoff_, hs_binbase_, ea);
       // B: bins -> sub-bins (tiles past the used ones exit; their counters stay zero)
       const size_t tiles = ((size_t)total_ + HS_TILE - 1) / HS_TILE + hs_nbins_;
       const size_t nh2 = tiles << hs_b2_;
@@ -726,7 +728,7 @@ void MsmPlan::build(const uint32_t* scalars, size_t n) {
     total_ = (uint32_t)(n * W);
     if (total_ > 0) {
       hipLaunchKernelGGL(k_digit_write_dense, dim3(grid_for(n)), dim3(TPB), 0, st, scalars, (uint32_t)n, prm_.c,
-                         (int)W, prm_.depth, nb, keys_, vals_);
+                         prm_.nb1, (int)W, prm_.depth, nb, keys_, vals_);
       size_t tmp = sort_tmp_bytes_;
       HIPX(sort_pairs(sort_tmp_, tmp, keys_, keys_sorted_, vals_, vals_sorted_, (size_t)total_, dense_bits_, st));
       hipLaunchKernelGGL(k_bounds, dim3(grid_for(total_)), dim3(TPB), 0, st, keys_sorted_, total_, bstart_, bend_);
@@ -739,12 +741,12 @@ void MsmPlan::build(const uint32_t* scalars, size_t n) {
     if (n > 0) {
       const uint32_t nblk = grid_for(n, TPB * BIN_R);
       const size_t nh = (size_t)nbins_ * nblk;
-      hipLaunchKernelGGL(k_bin_hist, dim3(nblk), dim3(TPB), 0, st, scalars, (uint32_t)n, prm_.c, (int)W, prm_.depth,
-                         fine_bits_, nbins_, hist_);
+      hipLaunchKernelGGL(k_bin_hist, dim3(nblk), dim3(TPB), 0, st, scalars, (uint32_t)n, prm_.c, prm_.nb1, (int)W,
+                         prm_.depth, fine_bits_, nbins_, hist_);
       HIPX(hipMemsetAsync(hist_ + nh, 0, 4, st));
       size_t stmp0 = scan_tmp_bytes_;
       HIPX(hipcub::DeviceScan::ExclusiveSum(scan_tmp_, stmp0, hist_, hoff_, (int)(nh + 1), st));
-      hipLaunchKernelGGL(k_bin_scatter, dim3(nblk), dim3(TPB), 0, st, scalars, (uint32_t)n, prm_.c, (int)W,
+      hipLaunchKernelGGL(k_bin_scatter, dim3(nblk), dim3(TPB), 0, st, scalars, (uint32_t)n, prm_.c, prm_.nb1, (int)W,
                          prm_.depth, fine_bits_, nbins_, hoff_, keys_, vals_);
       hipLaunchKernelGGL(k_chunk_count, dim3(grid_for(nbins_ + 1)), dim3(TPB), 0, st, hoff_, nblk, nbins_, nch_);
       size_t stmp1 = scan_tmp_bytes_;
@@ -766,11 +768,12 @@ void MsmPlan::build(const uint32_t* scalars, size_t n) {
   } else if (n > 0 && !use_wsort_) {
     // 1. digits, compacted: only nonzero digits, window-major, point order within a window
     const uint32_t nblk = grid_for(n);
-    hipLaunchKernelGGL(k_digit_count, dim3(nblk), dim3(TPB), 0, st, scalars, (uint32_t)n, prm_.c, (int)W, bcnt_);
+    hipLaunchKernelGGL(k_digit_count, dim3(nblk), dim3(TPB), 0, st, scalars, (uint32_t)n, prm_.c, prm_.nb1, (int)W,
+                       bcnt_);
     HIPX(hipMemsetAsync(bcnt_ + (size_t)W * nblk, 0, 4, st));
     size_t stmp0 = scan_tmp_bytes_;
     HIPX(hipcub::DeviceScan::ExclusiveSum(scan_tmp_, stmp0, bcnt_, boff_, (int)((size_t)W * nblk + 1), st));
-    hipLaunchKernelGGL(k_digit_write, dim3(nblk), dim3(TPB), 0, st, scalars, (uint32_t)n, prm_.c, (int)W,
+    hipLaunchKernelGGL(k_digit_write, dim3(nblk), dim3(TPB), 0, st, scalars, (uint32_t)n, prm_.c, prm_.nb1, (int)W,
                        prm_.depth, boff_, keys_, vals_);
     HIPX(hipMemcpyAsync(h_valid_, boff_ + (size_t)W * nblk, 4, hipMemcpyDeviceToHost, st));
     HIPX(hipStreamSynchronize(st));  // the sort needs the entry count on the host
@@ -871,8 +874,8 @@ void MsmEngine::accumulate(const MsmPlan& plan, const MsmBases& bases) {
   const MsmParams& p = plan.params();
   if (p.c != prm_.c || p.depth != prm_.depth || p.windows != prm_.windows)
     throw std::runtime_error("MSM: plan and engine parameters differ");
-  if (bases.c() != p.c || bases.depth() != p.depth || bases.curve() != curve_)
-    throw std::runtime_error("MSM: base table does not match the plan (c, depth, curve)");
+  if (bases.c() != p.c || bases.depth() != p.depth || bases.curve() != curve_ || bases.nb1() != p.nb1)
+    throw std::runtime_error("MSM: base table does not match the plan (c, depth, window widths, curve)");
   if (bases.n() != plan.n()) throw std::runtime_error("MSM: base table size differs from the scalar count");
   if (plan.n() > max_n_) throw std::runtime_error("MSM: n exceeds engine capacity");
   HIPX(hipStreamWaitEvent(stream_, plan.ready(), 0));

@@ -51,8 +51,12 @@ struct MsmParams {
   int S2 = 4;        // fan-in of a heavy-bucket merge level (short chains: latency-bound)
   int M = 4;         // buckets per reduction segment (running sums)
   int L = 8;         // fan-in of a subset-sum tree level
-  // c_override / depth_override: 0 = automatic
-  static MsmParams make(size_t n, int c_override = 0, int depth_override = 0) {
+  int nb1 = 255;     // windows 0..nb1-1 are c bits wide, the rest c-1 (>= windows: all c bits)
+  // c_override / depth_override: 0 = automatic.  balanced (only with depth == windows, one bucket
+  // group): the W windows split the 255 digit bits as nb1 x c + (W - nb1) x (c - 1), so the top window
+  // is not a narrow one whose n digits pile into its few low buckets (c = 20: 8 x 20 + 5 x 19 bits
+  // instead of 12 x 20 + 15; the (c-1)-bit windows use the lower half of the shared buckets)
+  static MsmParams make(size_t n, int c_override = 0, int depth_override = 0, bool balanced = false) {
     MsmParams p;
     int lg = 0;
     while ((size_t(1) << lg) < n) ++lg;
@@ -66,8 +70,13 @@ struct MsmParams {
     p.depth = depth_override > 0 ? (depth_override < p.windows ? depth_override : p.windows) : p.windows;
     p.groups = (p.windows + p.depth - 1) / p.depth;
     if (p.M > (1 << (p.c - 1))) p.M = 1 << (p.c - 1);
+    if (balanced && p.groups == 1 && p.c >= 3) {
+      const int nb = 255 - p.windows * (p.c - 1);
+      p.nb1 = nb < 0 ? 0 : (nb > p.windows ? p.windows : nb);
+    }
     return p;
   }
+  bool balanced() const { return nb1 < windows; }
   // reduction output: per group, lgP subset sums Q_b and sum_p T_p (P = 2^(c-1) / M segments)
   int lg_m() const { int l = 0; while ((1 << l) < M) ++l; return l; }
   int lgP() const { return c - 1 - lg_m(); }
@@ -102,7 +111,7 @@ inline int curve_fwords(Curve c) { return c == Curve::G1 ? 8 : 16; }
 // Precomputed base table: rows() x n affine points (device layout, Montgomery R'=2^261).
 class MsmBases {
  public:
-  MsmBases(Curve curve, size_t n, int c, int depth);
+  MsmBases(Curve curve, size_t n, int c, int depth, int nb1 = 255);
   ~MsmBases();
   MsmBases(const MsmBases&) = delete;
   MsmBases& operator=(const MsmBases&) = delete;
@@ -113,6 +122,7 @@ class MsmBases {
   size_t n() const { return n_; }
   int c() const { return c_; }
   int depth() const { return depth_; }
+  int nb1() const { return nb1_; }
   Curve curve() const { return curve_; }
   size_t bytes() const { return bytes_; }
   static size_t bytes_for(Curve curve, size_t n, int depth) {
@@ -122,7 +132,7 @@ class MsmBases {
  private:
   Curve curve_;
   size_t n_;
-  int c_, depth_;
+  int c_, depth_, nb1_;
   size_t bytes_ = 0;
   uint32_t* d_ = nullptr;
 };

@@ -34,11 +34,18 @@ ZDEV void load_scalar(const uint32_t* __restrict__ scalars, uint32_t i, uint32_t
   while (scalar_geq_r(s)) scalar_sub_r(s);
 }
 
-// signed c-bit digit of window w (windows visited in order, carry threaded through):
+// Window geometry: windows 0..nb1-1 are c bits wide, windows nb1.. are c-1 bits wide (nb1 >= W:
+// all c bits, the default).  "Balanced" widths (MsmParams::balanced) spread the 255 digit bits
+// evenly instead of leaving a narrow top window whose digits all fall into a few low buckets.
+ZDEV int win_bit(int w, int c, int nb1) { return w < nb1 ? w * c : nb1 * c + (w - nb1) * (c - 1); }
+ZDEV int win_width(int w, int c, int nb1) { return w < nb1 ? c : c - 1; }
+
+// signed digit of window w (windows visited in order, carry threaded through):
 // returns |d| (0 for a zero digit); neg = (d < 0)
-ZDEV uint32_t digit_mag(const uint32_t (&s)[9], int w, int c, uint32_t& carry, bool& neg) {
-  const uint32_t half = 1u << (c - 1), full = 1u << c;
-  const int bit = w * c, j = bit >> 5, sh = bit & 31;
+ZDEV uint32_t digit_mag(const uint32_t (&s)[9], int w, int c, int nb1, uint32_t& carry, bool& neg) {
+  const int wb = win_width(w, c, nb1);
+  const uint32_t half = 1u << (wb - 1), full = 1u << wb;
+  const int bit = win_bit(w, c, nb1), j = bit >> 5, sh = bit & 31;
   const uint64_t v = (uint64_t)s[j] | ((uint64_t)s[j + 1] << 32);  // sh + c <= 31 + 24 < 64
   const uint32_t raw = ((uint32_t)(v >> sh) & (full - 1)) + carry;
   if (raw > half) {
@@ -52,26 +59,27 @@ ZDEV uint32_t digit_mag(const uint32_t (&s)[9], int w, int c, uint32_t& carry, b
 }
 
 // entry of window w of scalar i: bucket key = group*2^(c-1) + |d|-1 with group = w / T,
-// base index (t*n + i) | sign with t = w % T (row t of the table holds 2^(c t) P_i)
-ZDEV bool digit_entry(const uint32_t (&s)[9], int w, int c, int T, uint32_t n, uint32_t i, uint32_t& carry,
-                      uint32_t& key, uint32_t& val) {
+// base index (t*n + i) | sign with t = w % T (row t of the table holds 2^(bit offset of window t) P_i)
+ZDEV bool digit_entry(const uint32_t (&s)[9], int w, int c, int nb1, int T, uint32_t n, uint32_t i,
+                      uint32_t& carry, uint32_t& key, uint32_t& val) {
   bool neg;
-  const uint32_t mag = digit_mag(s, w, c, carry, neg);
+  const uint32_t mag = digit_mag(s, w, c, nb1, carry, neg);
   const uint32_t g = (uint32_t)w / (uint32_t)T, t = (uint32_t)w - g * (uint32_t)T;
   key = (g << (c - 1)) + mag - 1;
   val = (t * n + i) | (neg ? 0x80000000u : 0u);
   return mag != 0;
 }
 
-// row t of base i from row t-1: 2^c * P (affine; infinity stays all-zero)
+// row t of base i from row t-1: 2^dbl * P, dbl = the width of window t - 1 (affine; infinity
+// stays all-zero)
 template <class F>
-ZDEV void extend_row(uint32_t i, uint32_t* __restrict__ table, uint32_t n, int c, int t) {
+ZDEV void extend_row(uint32_t i, uint32_t* __restrict__ table, uint32_t n, int dbl, int t) {
   if (i >= n) return;
   const Aff<F> p = load_aff<F>(table, (size_t)(t - 1) * n + i);
   Aff<F> a = p;
   if (!aff_is_inf(p)) {
     Xyzz<F> q = xyzz_dbl_aff(p);
-    for (int k = 1; k < c; ++k) q = xyzz_dbl(q);
+    for (int k = 1; k < dbl; ++k) q = xyzz_dbl(q);
     a = xyzz_to_aff(q);
   }
   store_aff(table, (size_t)t * n + i, a);

@@ -116,8 +116,11 @@ static void choose_msm_params(size_t n_w, size_t n_h, MsmParams& pw, MsmParams& 
   auto clampc = [](int c) { return c < 8 ? 8 : (c > 20 ? 20 : c); };
   const int c = env_int("ZKP_WINDOW_BITS", 0), d = env_int("ZKP_TABLE_DEPTH", 0);
   const int cw = env_int("ZKP_WINDOW_BITS_W", c ? c : clampc(lg(n_w) - 5));
-  // (the dense H plan avoids window widths whose top window collapses into a few buckets)
-  const int ch = env_int("ZKP_WINDOW_BITS_H", c ? c : dense_window_bits(clampc(lg(n_h) - 3), n_h));
+  // the H plan's windows: balanced widths (ZKP_H_BALANCED=1: nb1 x c + (W - nb1) x (c - 1) bits, no
+  // narrow top window), else uniform c-bit windows with c moved off the widths whose top window
+  // collapses into a few buckets (dense_window_bits)
+  const bool hbal = env_int("ZKP_H_BALANCED", 0) == 1;
+  const int ch = env_int("ZKP_WINDOW_BITS_H", c ? c : (hbal ? clampc(lg(n_h) - 3) : dense_window_bits(clampc(lg(n_h) - 3), n_h)));
   const int sw = env_int("ZKP_TASK_W", 0), sh = env_int("ZKP_TASK_H", 0);  // entries per task (tuning)
   // buckets per reduction segment / subset-sum fan-in (tuning; powers of two)
   const int sm = env_int("ZKP_SEG_M", 0), sl = env_int("ZKP_SUB_L", 0);
@@ -130,7 +133,7 @@ static void choose_msm_params(size_t n_w, size_t n_h, MsmParams& pw, MsmParams& 
     }
   };
   pw = MsmParams::make(n_w, cw, d);
-  ph = MsmParams::make(n_h, ch, d);
+  ph = MsmParams::make(n_h, ch, d, hbal);
   tasks();
   if (d > 0) return;
   size_t free_b = 0, total_b = 0;
@@ -141,7 +144,7 @@ static void choose_msm_params(size_t n_w, size_t n_h, MsmParams& pw, MsmParams& 
   while (depth > 1 && (size_t)std::min(depth, pw.windows) * row_w + (size_t)std::min(depth, ph.windows) * row_h > budget)
     --depth;
   pw = MsmParams::make(n_w, cw, depth);
-  ph = MsmParams::make(n_h, ch, depth);
+  ph = MsmParams::make(n_h, ch, depth, hbal);
   tasks();
 }
 
@@ -286,7 +289,7 @@ class DevicePipeline {
       tb1_ = std::make_shared<MsmBases>(Curve::G1, nv, pw.c, pw.depth);
       tc_ = std::make_shared<MsmBases>(Curve::G1, nv, pw.c, pw.depth);
       tb2_ = std::make_shared<MsmBases>(Curve::G2, nv, pw.c, pw.depth);
-      th_ = std::make_shared<MsmBases>(Curve::G1, nd, ph.c, ph.depth);
+      th_ = std::make_shared<MsmBases>(Curve::G1, nd, ph.c, ph.depth, ph.nb1);
       fill_bases(*ta_, z.bf.sec[5].ptr + wlo_ * 64, nv, 0, s0_);
       fill_bases(*tb1_, z.bf.sec[6].ptr + wlo_ * 64, nv, 0, s0_);
       fill_bases(*tb2_, z.bf.sec[7].ptr + wlo_ * 128, nv, 0, s0_);
@@ -1294,9 +1297,11 @@ struct MsmRig {
       // c = lg n - 4.  ZKP_MSM_C / ZKP_MSM_DENSE=0 override (A/B).
       int lg = 0;
       while ((size_t(1) << lg) < n) ++lg;
-      const int c_auto = env_int("ZKP_MSM_C", dense_window_bits(std::min(20, std::max(8, lg - 3)), n));
-      prm = MsmParams::make(std::max<size_t>(n, 1), c ? c : c_auto, depth);
-      bases = std::make_unique<MsmBases>(curve, n, prm.c, prm.depth);
+      const bool bal = env_int("ZKP_MSM_BALANCED", env_int("ZKP_H_BALANCED", 0)) == 1;  // as the H plan
+      const int c_raw = std::min(20, std::max(8, lg - 3));
+      const int c_auto = env_int("ZKP_MSM_C", bal ? c_raw : dense_window_bits(c_raw, n));
+      prm = MsmParams::make(std::max<size_t>(n, 1), c ? c : c_auto, depth, bal);
+      bases = std::make_unique<MsmBases>(curve, n, prm.c, prm.depth, prm.nb1);
       fill_bases(*bases, points, n, 0, st);
       plan = std::make_unique<MsmPlan>(std::max<size_t>(n, 1), prm, st);
       plan->set_dense(env_int("ZKP_MSM_DENSE", 1) != 0);
@@ -1409,7 +1414,7 @@ float bench_plan(int device, const uint8_t* scalars, size_t n, int c, int dense,
   try {
     HIPX(hipEventCreate(&e0));
     HIPX(hipEventCreate(&e1));
-    const MsmParams prm = MsmParams::make(n, c, 0);
+    const MsmParams prm = MsmParams::make(n, c, 0, env_int("ZKP_MSM_BALANCED", 0) == 1 && dense);
     MsmPlan plan(n, prm, st);
     plan.set_dense(dense != 0);
     HIPX(hipMalloc(&d, n * 32));

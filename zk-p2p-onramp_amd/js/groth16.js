@@ -9,7 +9,9 @@
  * same Error messages (from the C ABI).  The zkey is loaded once per process and stays
  * resident in HBM (snarkjs re-reads it on every call): a path zkey is keyed by its path, a
  * memory zkey ({type:"mem"} / Buffer, the fullProve / fastfile path) by the SHA-256 of its
- * bytes, so repeated proofs with the same in-memory key reuse the resident handle.  There is
+ * bytes, so repeated proofs with the same in-memory key reuse the resident handle.  The hash is
+ * computed once per key buffer (a WeakMap on the underlying ArrayBuffer remembers it), not on
+ * every call: a GB-scale key would otherwise block the event loop for ~1 s per proof.  There is
  * no CPU fallback: if the native addon or libzkp_amd.so is missing, require() throws.
  */
 const crypto = require('crypto');
@@ -20,6 +22,7 @@ const addon = require(path.join(__dirname, 'build', 'zkp_napi.node'));
 const provers = new Map();     // zkey path -> handle
 const memProvers = new Map();  // sha256(zkey bytes) -> handle, most recently used last
 const MEM_PROVERS_MAX = 2;     // each holds its key's base tables in HBM (~50 GB for Venmo)
+const memKeyHash = new WeakMap();  // ArrayBuffer -> [{off, len, hash}] of key buffers already hashed
 
 function readInput(x) {
   if (x && typeof x === 'object' && x.type === 'mem') return Buffer.from(x.data.buffer ? x.data : Buffer.from(x.data));
@@ -36,8 +39,18 @@ function proverFor(zkey, devices) {
     }
     return h;
   }
-  const buf = readInput(zkey);
-  const key = crypto.createHash('sha256').update(buf).digest('hex') + ':' + JSON.stringify(devices || []);
+  const src = zkey && typeof zkey === 'object' && zkey.type === 'mem' ? zkey.data : zkey;
+  const buf = ArrayBuffer.isView(src) ? Buffer.from(src.buffer, src.byteOffset, src.byteLength) : readInput(zkey);
+  let seen = ArrayBuffer.isView(src) ? memKeyHash.get(src.buffer) : undefined;
+  let hit = seen && seen.find((e) => e.off === src.byteOffset && e.len === src.byteLength);
+  if (!hit) {
+    hit = { off: buf.byteOffset, len: buf.byteLength, hash: crypto.createHash('sha256').update(buf).digest('hex') };
+    if (ArrayBuffer.isView(src)) {
+      if (!seen) memKeyHash.set(src.buffer, (seen = []));
+      seen.push(hit);
+    }
+  }
+  const key = hit.hash + ':' + JSON.stringify(devices || []);
   let h = memProvers.get(key);
   if (h) {
     memProvers.delete(key);  // refresh its LRU position
