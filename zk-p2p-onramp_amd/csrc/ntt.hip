@@ -136,13 +136,20 @@ __device__ __forceinline__ int swz(int e) {
   return e ^ ((h ^ (h << 1) ^ (h << 3)) & 31);
 }
 
-__device__ __forceinline__ Fr lds_get(const uint32_t* __restrict__ lds, int E, int e) {
+// LDS tile access: lds[limb * E + element].  With a compile-time E (LE > 0: the 1024-element tiles of
+// every transform of 2^10 points or more) limb l is a constant byte offset l * 4E of one address
+// register (ds_read2st64 pairs), instead of nine address registers and adds per element per round.
+template <int LE>
+__device__ __forceinline__ Fr lds_get(const uint32_t* __restrict__ lds, int E_rt, int e) {
+  const int E = LE ? (1 << LE) : E_rt;
   Fr x;
 #pragma unroll
   for (int l = 0; l < NL; ++l) x.v[l] = lds[l * E + e];
   return x;
 }
-__device__ __forceinline__ void lds_put(uint32_t* __restrict__ lds, int E, int e, const Fr& x) {
+template <int LE>
+__device__ __forceinline__ void lds_put(uint32_t* __restrict__ lds, int E_rt, int e, const Fr& x) {
+  const int E = LE ? (1 << LE) : E_rt;
 #pragma unroll
   for (int l = 0; l < NL; ++l) lds[l * E + e] = x.v[l];
 }
@@ -182,8 +189,10 @@ __device__ __forceinline__ Fr bfly_d(const Fr& x, const Fr& y, const uint32_t* _
 // b radix-2 DIF stages on the LDS tile (rows natural in, bit-reversed out), done two at a
 // time as radix-4 groups in registers (half the LDS traffic and barriers of radix-2):
 // rows r0 + {0, H/2, H, 3H/2} of stage t (span H) and t+1 (span H/2), r0 = grp 2H + i.
-__device__ __forceinline__ void dft_stages(uint32_t* __restrict__ lds, const uint32_t* __restrict__ ltw, int E, int b,
+template <int LE>
+__device__ __forceinline__ void dft_stages(uint32_t* __restrict__ lds, const uint32_t* __restrict__ ltw, int E_rt, int b,
                                            int lc) {
+  const int E = LE ? (1 << LE) : E_rt;
   const uint32_t C = 1u << lc;
   int t = 0;
   for (; t + 1 < b; t += 2) {
@@ -198,7 +207,7 @@ __device__ __forceinline__ void dft_stages(uint32_t* __restrict__ lds, const uin
       const int st = (int)(Hh << lc);
       // swizzled rows e0 + k st = e0 | k st (disjoint bits): p0 ^ swz(k st)
       const int p0 = swz(base + (int)(r0 << lc)), p1 = p0 ^ swz(st), p2 = p0 ^ swz(2 * st), p3 = p0 ^ swz(3 * st);
-      const Fr x0 = lds_get(lds, E, p0), x1 = lds_get(lds, E, p1), x2 = lds_get(lds, E, p2), x3 = lds_get(lds, E, p3);
+      const Fr x0 = lds_get<LE>(lds, E, p0), x1 = lds_get<LE>(lds, E, p1), x2 = lds_get<LE>(lds, E, p2), x3 = lds_get<LE>(lds, E, p3);
       // stage t: (x0, x2) with w_(2H)^i, (x1, x3) with w_(2H)^(i + H/2); stage t+1: (s02, s13)
       // and (d02, d13), both with w_H^i.  Roots as exponents of w_(2^b) (stage t: i << t).
 #if ZKP_NTT_MUL2
@@ -211,18 +220,18 @@ __device__ __forceinline__ void dft_stages(uint32_t* __restrict__ lds, const uin
         Fr y0, y1, y2, y3;
         r4_dif(x0, x1, x2, x3, root(ltw, ia), root(ltw, ib), root(ltw, ic), root(ltw, id), root(ltw, i << (t + 1)),
                y0, y1, y2, y3);
-        lds_put(lds, E, p0, y0);
-        lds_put(lds, E, p1, y1);
-        lds_put(lds, E, p2, y2);
-        lds_put(lds, E, p3, y3);
+        lds_put<LE>(lds, E, p0, y0);
+        lds_put<LE>(lds, E, p1, y1);
+        lds_put<LE>(lds, E, p2, y2);
+        lds_put<LE>(lds, E, p3, y3);
       } else {  // last pair (span 1, i = 0): roots 1 except w_(2H)^(H/2) for (x1, x3)
         const Fr d02 = sub(x0, x2);
         const Fr d13 = mul(rsub(x1, x3), root(ltw, Hh << t));
         const Fr s02 = add(x0, x2), s13 = add(x1, x3);
-        lds_put(lds, E, p0, add(s02, s13));
-        lds_put(lds, E, p1, sub(s02, s13));
-        lds_put(lds, E, p2, add(d02, d13));
-        lds_put(lds, E, p3, sub(d02, d13));
+        lds_put<LE>(lds, E, p0, add(s02, s13));
+        lds_put<LE>(lds, E, p1, sub(s02, s13));
+        lds_put<LE>(lds, E, p2, add(d02, d13));
+        lds_put<LE>(lds, E, p3, sub(d02, d13));
       }
 #else
       const Fr d02 = bfly_d(x0, x2, ltw, i << t);
@@ -230,15 +239,15 @@ __device__ __forceinline__ void dft_stages(uint32_t* __restrict__ lds, const uin
       const uint32_t j = i << (t + 1);
       if (Hh > 1) {  // the sums stay raw (< 4m) and meet one reduction; w_H^0 = 1 (Montgomery) for i = 0
         const Fr s02 = add_raw(x0, x2), s13 = add_raw(x1, x3);
-        lds_put(lds, E, p0, add_raw_reduce(s02, s13));
-        lds_put(lds, E, p1, root_mul(sub_raw6(s02, s13), ltw, j));
+        lds_put<LE>(lds, E, p0, add_raw_reduce(s02, s13));
+        lds_put<LE>(lds, E, p1, root_mul(sub_raw6(s02, s13), ltw, j));
       } else {  // last pair (span 1): no multiply in stage t+1
         const Fr s02 = add(x0, x2), s13 = add(x1, x3);
-        lds_put(lds, E, p0, add(s02, s13));
-        lds_put(lds, E, p1, sub(s02, s13));
+        lds_put<LE>(lds, E, p0, add(s02, s13));
+        lds_put<LE>(lds, E, p1, sub(s02, s13));
       }
-      lds_put(lds, E, p2, add(d02, d13));
-      lds_put(lds, E, p3, bfly_d(d02, d13, ltw, j));
+      lds_put<LE>(lds, E, p2, add(d02, d13));
+      lds_put<LE>(lds, E, p3, bfly_d(d02, d13, ltw, j));
 #endif
     }
     __syncthreads();
@@ -248,9 +257,9 @@ __device__ __forceinline__ void dft_stages(uint32_t* __restrict__ lds, const uin
       const uint32_t col = (uint32_t)q & (C - 1), bq = ((uint32_t)q >> lc) & ((1u << (b - 1)) - 1);
       const uint32_t bl = (uint32_t)q >> (lc + b - 1);
       const int p0 = swz((int)(bl << (b + lc)) + (int)((bq << 1) << lc) + (int)col), p1 = p0 ^ swz((int)C);
-      const Fr x = lds_get(lds, E, p0), y = lds_get(lds, E, p1);
-      lds_put(lds, E, p0, add(x, y));
-      lds_put(lds, E, p1, stage_sub(x, y));  // span 1: the root is w_2^0 = 1
+      const Fr x = lds_get<LE>(lds, E, p0), y = lds_get<LE>(lds, E, p1);
+      lds_put<LE>(lds, E, p0, add(x, y));
+      lds_put<LE>(lds, E, p1, stage_sub(x, y));  // span 1: the root is w_2^0 = 1
     }
     __syncthreads();
   }
@@ -293,14 +302,14 @@ __device__ __forceinline__ int brev_src(const Tile& T, int e) {
 #else
 #define NTT_WPE_ATTR
 #endif
-template <int MODE>
+template <int MODE, int LE>
 __global__ __launch_bounds__(TPB) NTT_WPE_ATTR void k_ntt(uint32_t* __restrict__ data, Tile T, const uint32_t* __restrict__ tw,
                                              const uint32_t* __restrict__ rootsA, const uint32_t* __restrict__ rootsB,
                                              const uint32_t* __restrict__ locA, const uint32_t* __restrict__ locB,
                                              const uint32_t* __restrict__ coset) {
   __shared__ uint32_t lds[NL << LOG_TILE];  // SoA: lds[limb * E + element]
   __shared__ __attribute__((aligned(16))) uint32_t ltw[RW * MAX_TW];
-  const int E = 1 << (T.b + T.lc + T.lbt);
+  const int E = LE ? (1 << LE) : (1 << (T.b + T.lc + T.lbt));  // LE: the tile size known at compile time
   const uint32_t tile = blockIdx.x;
   stage_roots(ltw, rootsA, locA, T.b);
   for (int e = threadIdx.x; e < E; e += TPB) {
@@ -313,31 +322,39 @@ __global__ __launch_bounds__(TPB) NTT_WPE_ATTR void k_ntt(uint32_t* __restrict__
     for (int l = 0; l < NL; ++l) lds[l * E + swz(e)] = x.v[l];
   }
   __syncthreads();
-  dft_stages(lds, ltw, E, T.b, T.lc);
+  dft_stages<LE>(lds, ltw, E, T.b, T.lc);
   if (MODE == 2) {
     // output row k1 (natural position in the block) sits at LDS row brev(k1): key it with
     // g^f(pos)/n and put it back at row k1 as the forward DFT's input
-    Fr v[(1 << LOG_TILE) / TPB];
-    int idx = 0;
-    for (int e = threadIdx.x; e < E; e += TPB, ++idx) {
-      const int src = swz(brev_src(T, e));
-      Fr x;
+    // (a fixed trip count keeps v[] in registers: a runtime-indexed array went to scratch)
+    constexpr int VPT = (1 << LOG_TILE) / TPB;
+    Fr v[VPT];
 #pragma unroll
-      for (int l = 0; l < NL; ++l) x.v[l] = lds[l * E + src];
-      size_t g;
-      uint32_t pos;
-      tile_coords(T, tile, e, g, pos);
-      v[idx] = mul(x, load_fe<FrCfg>(coset + g * 8));
+    for (int it = 0; it < VPT; ++it) {
+      const int e = (int)threadIdx.x + it * TPB;
+      if (e < E) {
+        const int src = swz(brev_src(T, e));
+        Fr x;
+#pragma unroll
+        for (int l = 0; l < NL; ++l) x.v[l] = lds[l * E + src];
+        size_t g;
+        uint32_t pos;
+        tile_coords(T, tile, e, g, pos);
+        v[it] = mul(x, load_fe<FrCfg>(coset + g * 8));
+      }
     }
     __syncthreads();
     stage_roots(ltw, rootsB, locB, T.b);  // the forward roots replace the inverse ones (no reader until the next barrier)
-    idx = 0;
-    for (int e = threadIdx.x; e < E; e += TPB, ++idx) {
 #pragma unroll
-      for (int l = 0; l < NL; ++l) lds[l * E + swz(e)] = v[idx].v[l];
+    for (int it = 0; it < VPT; ++it) {
+      const int e = (int)threadIdx.x + it * TPB;
+      if (e < E) {
+#pragma unroll
+        for (int l = 0; l < NL; ++l) lds[l * E + swz(e)] = v[it].v[l];
+      }
     }
     __syncthreads();
-    dft_stages(lds, ltw, E, T.b, T.lc);
+    dft_stages<LE>(lds, ltw, E, T.b, T.lc);
   }
   for (int e = threadIdx.x; e < E; e += TPB) {
     const int src = swz(brev_src(T, e));
@@ -574,15 +591,20 @@ void NttEngine::launch_pass(uint32_t* data, int mode, int p, bool inv) {
   const uint32_t *ra = rt ? rtab_[d][T.b] : nullptr, *rinv = rt ? rtab_[1][T.b] : nullptr,
                  *rfwd = rt ? rtab_[0][T.b] : nullptr;
   const uint32_t* none = nullptr;
+  // full 1024-element tiles (every transform of 2^10 points or more) take the compile-time tile size
+  const bool full = T.b + T.lc + T.lbt == LOG_TILE;
+  auto k0 = full ? k_ntt<0, LOG_TILE> : k_ntt<0, 0>;
+  auto k1 = full ? k_ntt<1, LOG_TILE> : k_ntt<1, 0>;
+  auto k2 = full ? k_ntt<2, LOG_TILE> : k_ntt<2, 0>;
   if (mode == 0)
-    hipLaunchKernelGGL(k_ntt<0>, dim3((unsigned)tiles), dim3(TPB), 0, stream_, data, T, tw_pass_[d][p], ra, none,
-                       loc_[d], none, none);
+    hipLaunchKernelGGL(k0, dim3((unsigned)tiles), dim3(TPB), 0, stream_, data, T, tw_pass_[d][p], ra, none, loc_[d],
+                       none, none);
   else if (mode == 1)
-    hipLaunchKernelGGL(k_ntt<1>, dim3((unsigned)tiles), dim3(TPB), 0, stream_, data, T, tw_pass_[d][p], ra, none,
-                       loc_[d], none, none);
+    hipLaunchKernelGGL(k1, dim3((unsigned)tiles), dim3(TPB), 0, stream_, data, T, tw_pass_[d][p], ra, none, loc_[d],
+                       none, none);
   else
-    hipLaunchKernelGGL(k_ntt<2>, dim3((unsigned)tiles), dim3(TPB), 0, stream_, data, T, none, rinv, rfwd, loc_[1],
-                       loc_[0], coset_pos_);
+    hipLaunchKernelGGL(k2, dim3((unsigned)tiles), dim3(TPB), 0, stream_, data, T, none, rinv, rfwd, loc_[1], loc_[0],
+                       coset_pos_);
 }
 
 void NttEngine::dif_passes(uint32_t* data, bool inv, int first, int last) {

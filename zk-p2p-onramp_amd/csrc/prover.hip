@@ -552,14 +552,19 @@ class DevicePipeline {
     return prove_uploaded(slot.k, ms, early);
   }
 
-  MsmOut prove_staged(int slot, const EarlyFn& early = {}) {
+  MsmOut prove_staged(int slot, const EarlyFn& early = {}) { return prove_resident(slot_ptr(slot), early); }
+
+  // a proof of a witness already resident on this GPU: this pipeline's staging slot, or a
+  // ZKP_INFLIGHT sibling's (staged witnesses live in the device's first pipeline)
+  MsmOut prove_resident(const uint32_t* d_wit, const EarlyFn& early = {}) {
     std::lock_guard<std::mutex> lk(mu_);
     HIPX(hipSetDevice(dev_));
-    const uint32_t* d = slot_ptr(slot);
     HIPX(hipEventRecord(ev_[0], s0_));
     HIPX(hipEventRecord(ev_[1], s0_));
-    return prove_dev(d, early);
+    return prove_dev(d_wit, early);
   }
+  // claimed by a staged caller (Prover::prove_staged spreads concurrent callers over the pipelines)
+  std::atomic<bool> staged_busy{false};
 
   // the whole device pipeline on a resident witness (caller holds mu_, ev_[0..1] recorded)
   MsmOut prove_dev(const uint32_t* d_wit, const EarlyFn& early = {}) {
@@ -1225,11 +1230,29 @@ void Prover::stage(int dev, int slot, const uint8_t* wtns, size_t len) {
 
 void Prover::prove_staged(int dev, int slot, const uint8_t* r32, const uint8_t* s32, zkp_proof* out) {
   require_full();
-  DevicePipeline& d = staged_pipeline(dev);
+  DevicePipeline& base = staged_pipeline(dev);
+  const uint32_t* d_wit = base.slot_ptr(slot);
+  // concurrent staged callers on one device take its idle ZKP_INFLIGHT pipelines (the staged
+  // witnesses live in the first one; the others read them in place); with none idle the call
+  // queues on the first pipeline
+  DevicePipeline* d = &base;
+  bool claimed = false;
+  for (int k = 0; k < inflight_ && !claimed; ++k) {
+    DevicePipeline* c = devs_[(size_t)dev * inflight_ + k].get();
+    bool idle = false;
+    if (c->staged_busy.compare_exchange_strong(idle, true)) d = c, claimed = true;
+  }
+  struct Release {
+    DevicePipeline* d;
+    bool on;
+    ~Release() {
+      if (on) d->staged_busy.store(false);
+    }
+  } release{d, claimed};
   auto t0 = std::chrono::steady_clock::now();
   Blinded bl;
-  DevicePipeline::MsmOut m = d.prove_staged(
-      slot, [&](const DevicePipeline::MsmOut& o) { bl = assemble_pre(hdr_, o, r32, s32); });
+  DevicePipeline::MsmOut m = d->prove_resident(
+      d_wit, [&](const DevicePipeline::MsmOut& o) { bl = assemble_pre(hdr_, o, r32, s32); });
   auto t1 = std::chrono::steady_clock::now();
   WtnsView w;
   {
