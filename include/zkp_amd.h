@@ -245,8 +245,10 @@ zkp_status zkp_quotient(zkp_prover* p, const uint8_t* wtns, size_t len, uint8_t*
 /* ---- benchmarking / serving helpers ----
  * Keep a witness resident in HBM (dev_index: index into the `devices` list the prover was
  * loaded with, 0..ndev-1, whatever ZKP_INFLIGHT is; the witness goes to that device's first
- * pipeline; any slot number); zkp_prove_staged then runs the proof without the PCIe copy on
- * the same pipeline.  Calls for different dev_index values run concurrently. */
+ * pipeline; any slot number); zkp_prove_staged then runs the proof without the PCIe copy.
+ * Calls for different dev_index values run concurrently; concurrent calls for the same
+ * dev_index take that device's idle ZKP_INFLIGHT pipelines (which read the staged witness in
+ * place) and queue on its first pipeline when none is idle. */
 zkp_status zkp_witness_stage(zkp_prover* p, int dev_index, int slot, const uint8_t* wtns, size_t len);
 zkp_status zkp_prove_staged(zkp_prover* p, int dev_index, int slot, const uint8_t* r32, const uint8_t* s32,
                             zkp_proof* out);
