@@ -25,19 +25,23 @@ struct Xyzz {
   F x, y, zz, zzz;
 };
 
+// zero / one of a base field (any Fe<C>: Fq, or Fq as the accumulation computes it) or of Fq2
 template <class F>
-ZDEV F f_zero();
+struct FConst;
+template <class C>
+struct FConst<Fe<C>> {
+  static ZDEV Fe<C> zero() { return fe_zero<C>(); }
+  static ZDEV Fe<C> one() { return fe_one<C>(); }
+};
 template <>
-ZDEV Fq f_zero<Fq>() { return fe_zero<FqCfg>(); }
-template <>
-ZDEV Fq2 f_zero<Fq2>() { return Fq2{fe_zero<FqCfg>(), fe_zero<FqCfg>()}; }
-
+struct FConst<Fq2> {
+  static ZDEV Fq2 zero() { return Fq2{fe_zero<FqCfg>(), fe_zero<FqCfg>()}; }
+  static ZDEV Fq2 one() { return Fq2{fe_one<FqCfg>(), fe_zero<FqCfg>()}; }
+};
 template <class F>
-ZDEV F f_one();
-template <>
-ZDEV Fq f_one<Fq>() { return fe_one<FqCfg>(); }
-template <>
-ZDEV Fq2 f_one<Fq2>() { return Fq2{fe_one<FqCfg>(), fe_zero<FqCfg>()}; }
+ZDEV F f_zero() { return FConst<F>::zero(); }
+template <class F>
+ZDEV F f_one() { return FConst<F>::one(); }
 
 // Accumulator-coordinate forms: the XYZZ additions keep x and the differences lazily reduced.
 //  G1: x < 8m (field.hpp sub_2x8: no conditional subtraction), differences with x via lsub8
@@ -47,20 +51,27 @@ ZDEV Fq2 f_one<Fq2>() { return Fq2{fe_one<FqCfg>(), fe_zero<FqCfg>()}; }
 //      without conditional subtractions, squares of such values by sqr_lazy; the Y3 sum of
 //      products puts the < 6m factor first (Fq2 mul2 negates the SECOND factor's c1, which must
 //      stay <= 4m).  Bounds: field.hpp, host-tested (tools/hosttest).
-ZDEV Fq acc_x3(const Fq& rr, const Fq& ppp, const Fq& q) { return sub_2x8(rr, ppp, q); }
+template <class C>
+ZDEV Fe<C> acc_x3(const Fe<C>& rr, const Fe<C>& ppp, const Fe<C>& q) { return sub_2x8(rr, ppp, q); }
 ZDEV Fq2 acc_x3(const Fq2& rr, const Fq2& ppp, const Fq2& q) { return sub_2x4(rr, ppp, q); }
-ZDEV Fq acc_xsub(const Fq& a, const Fq& x) { return lsub8(a, x); }  // a - x for an accumulator x
+template <class C>
+ZDEV Fe<C> acc_xsub(const Fe<C>& a, const Fe<C>& x) { return lsub8(a, x); }  // a - x for an accumulator x
 ZDEV Fq2 acc_xsub(const Fq2& a, const Fq2& x) { return lsub4_lazy(a, x); }
-ZDEV Fq acc_sub(const Fq& a, const Fq& b) { return lsub(a, b); }  // a - b, both < 2m
+template <class C>
+ZDEV Fe<C> acc_sub(const Fe<C>& a, const Fe<C>& b) { return lsub(a, b); }  // a - b, both < 2m
 ZDEV Fq2 acc_sub(const Fq2& a, const Fq2& b) { return lsub2_lazy(a, b); }
-ZDEV Fq acc_sqr(const Fq& a) { return sqr(a); }  // a < 11m
+template <class C>
+ZDEV Fe<C> acc_sqr(const Fe<C>& a) { return sqr(a); }  // a < 11m
 ZDEV Fq2 acc_sqr(const Fq2& a) { return sqr_lazy(a); }  // components < 6m
-ZDEV Fq acc_negd(const Fq& a) { return rsub(fe_zero<FqCfg>(), a); }
+template <class C>
+ZDEV Fe<C> acc_negd(const Fe<C>& a) { return rsub(fe_zero<C>(), a); }
 ZDEV Fq2 acc_negd(const Fq2& a) { return lsub2_lazy(Fq2{fe_zero<FqCfg>(), fe_zero<FqCfg>()}, a); }
 // Y3 = R T + Y D (T = Q - X3, D = -PPP)
-ZDEV Fq acc_y3(const Fq& r, const Fq& t, const Fq& y, const Fq& d) { return mul2(r, t, y, d); }
+template <class C>
+ZDEV Fe<C> acc_y3(const Fe<C>& r, const Fe<C>& t, const Fe<C>& y, const Fe<C>& d) { return mul2(r, t, y, d); }
 ZDEV Fq2 acc_y3(const Fq2& r, const Fq2& t, const Fq2& y, const Fq2& d) { return mul2(t, r, d, y); }
-ZDEV Fq acc_xcanon(const Fq& x) { return canon8(x); }
+template <class C>
+ZDEV Fe<C> acc_xcanon(const Fe<C>& x) { return canon8(x); }
 ZDEV Fq2 acc_xcanon(const Fq2& x) { return canon4(x); }
 
 template <class F>
@@ -254,12 +265,14 @@ ZDEV Aff<F> xyzz_to_aff(const Xyzz<F>& p) {
 // G1 affine: 16 words (x, y), each 8 LE words.  G2 affine: 32 words (x.c0, x.c1, y.c0, y.c1).
 // XYZZ: 4 coordinates in the same order.
 
-ZDEV void load_f(const uint32_t* p, Fq& x) { x = load_fe<FqCfg>(p); }
+template <class C>
+ZDEV void load_f(const uint32_t* p, Fe<C>& x) { x = load_fe<C>(p); }
 ZDEV void load_f(const uint32_t* p, Fq2& x) {
   x.c0 = load_fe<FqCfg>(p);
   x.c1 = load_fe<FqCfg>(p + 8);
 }
-ZDEV void store_f(uint32_t* p, const Fq& x) { store_fe(p, x); }
+template <class C>
+ZDEV void store_f(uint32_t* p, const Fe<C>& x) { store_fe(p, x); }
 ZDEV void store_f(uint32_t* p, const Fq2& x) {
   store_fe(p, x.c0);
   store_fe(p + 8, x.c1);
@@ -267,8 +280,8 @@ ZDEV void store_f(uint32_t* p, const Fq2& x) {
 
 template <class F>
 struct FWords;
-template <>
-struct FWords<Fq> {
+template <class C>
+struct FWords<Fe<C>> {
   static constexpr int W = 8;
 };
 template <>

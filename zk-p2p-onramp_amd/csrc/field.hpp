@@ -37,6 +37,40 @@ using Fr = Fe<FrCfg>;
 
 #define ZDEV __host__ __device__ __forceinline__
 
+// acc += x * y.  CH (C::CHAIN, device code): one v_mad_u64_u32 in inline assembly, so every product
+// column stays ONE dependent chain seeded by the previous column's carry.  Left to itself the
+// compiler re-associates each column into a sum from 0 plus a 64-bit join of the carry
+// (v_lshl_add_u64 per column); the chain form drops the joins, and the wait states between
+// dependent 64-bit mads (filled with s_nop) cost no VALU issue slot when other waves are ready:
+// 172 -> 183 G products/s at high occupancy (tools/ubench/mul_chain.hip, profiles/mul_chain_r03.txt),
+// slower where few waves hide them.  mac_k takes a constant (an SGPR operand).  ZKP_ASM_MAC=0
+// disables the assembly everywhere; host code is always plain C.
+#ifndef ZKP_ASM_MAC
+#define ZKP_ASM_MAC 1
+#endif
+template <bool CH>
+ZDEV void mac(uint64_t& acc, uint32_t x, uint32_t y) {
+#if ZKP_ASM_MAC && defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (CH) {
+    uint64_t cc;
+    asm("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc), "=s"(cc) : "v"(x), "v"(y));
+    return;
+  }
+#endif
+  acc += (uint64_t)x * y;
+}
+template <bool CH>
+ZDEV void mac_k(uint64_t& acc, uint32_t x, uint32_t k) {
+#if ZKP_ASM_MAC && defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (CH) {
+    uint64_t cc;
+    asm("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc), "=s"(cc) : "v"(x), "s"(k));
+    return;
+  }
+#endif
+  acc += (uint64_t)x * k;
+}
+
 template <class C>
 ZDEV Fe<C> fe_zero() {
   Fe<C> r;
@@ -67,20 +101,20 @@ ZDEV Fe<C> mul(const Fe<C>& a, const Fe<C>& b) {
   for (int i = 0; i < NL; ++i) {
 #pragma unroll
     for (int j = 0; j < i; ++j) {
-      acc += (uint64_t)a.v[j] * b.v[i - j];
-      acc += (uint64_t)m[j] * C::MOD[i - j];
+      mac<C::CHAIN>(acc, a.v[j], b.v[i - j]);
+      mac_k<C::CHAIN>(acc, m[j], C::MOD[i - j]);
     }
-    acc += (uint64_t)a.v[i] * b.v[0];
+    mac<C::CHAIN>(acc, a.v[i], b.v[0]);
     m[i] = ((uint32_t)acc * C::INV) & LMASK;
-    acc += (uint64_t)m[i] * C::MOD[0];
+    mac_k<C::CHAIN>(acc, m[i], C::MOD[0]);
     acc >>= LB;
   }
 #pragma unroll
   for (int i = NL; i < 2 * NL - 1; ++i) {
 #pragma unroll
     for (int j = i - NL + 1; j < NL; ++j) {
-      acc += (uint64_t)a.v[j] * b.v[i - j];
-      acc += (uint64_t)m[j] * C::MOD[i - j];
+      mac<C::CHAIN>(acc, a.v[j], b.v[i - j]);
+      mac_k<C::CHAIN>(acc, m[j], C::MOD[i - j]);
     }
     r.v[i - NL] = (uint32_t)acc & LMASK;
     acc >>= LB;
@@ -104,8 +138,7 @@ ZDEV Fe<C> mul_shoup(const Fe<C>& a, const Fe<C>& w, const Fe<C>& wq) {
 #pragma unroll
   for (int c = 7; c < 2 * NL - 1; ++c) {
 #pragma unroll
-    for (int i = (c - NL + 1 > 0 ? c - NL + 1 : 0); i <= (c < NL - 1 ? c : NL - 1); ++i)
-      acc += (uint64_t)a.v[i] * wq.v[c - i];
+    for (int i = (c - NL + 1 > 0 ? c - NL + 1 : 0); i <= (c < NL - 1 ? c : NL - 1); ++i) mac<C::CHAIN>(acc, a.v[i], wq.v[c - i]);
     if (c >= NL) q[c - NL] = (uint32_t)acc & LMASK;
     acc >>= LB;
   }
@@ -116,8 +149,8 @@ ZDEV Fe<C> mul_shoup(const Fe<C>& a, const Fe<C>& w, const Fe<C>& wq) {
   for (int c = 0; c < NL; ++c) {
 #pragma unroll
     for (int i = 0; i <= c; ++i) {
-      acc += (uint64_t)a.v[i] * w.v[c - i];
-      acc += (uint64_t)q[i] * C::NM[c - i];
+      mac<C::CHAIN>(acc, a.v[i], w.v[c - i]);
+      mac_k<C::CHAIN>(acc, q[i], C::NM[c - i]);
     }
     r.v[c] = (uint32_t)acc & LMASK;
     acc >>= LB;
@@ -164,23 +197,23 @@ ZDEV Fe<C> mul2(const Fe<C>& a, const Fe<C>& b, const Fe<C>& c, const Fe<C>& d) 
   for (int i = 0; i < NL; ++i) {
 #pragma unroll
     for (int j = 0; j < i; ++j) {
-      acc += (uint64_t)a.v[j] * b.v[i - j];
-      acc += (uint64_t)c.v[j] * d.v[i - j];
-      acc += (uint64_t)m[j] * C::MOD[i - j];
+      mac<C::CHAIN>(acc, a.v[j], b.v[i - j]);
+      mac<C::CHAIN>(acc, c.v[j], d.v[i - j]);
+      mac_k<C::CHAIN>(acc, m[j], C::MOD[i - j]);
     }
-    acc += (uint64_t)a.v[i] * b.v[0];
-    acc += (uint64_t)c.v[i] * d.v[0];
+    mac<C::CHAIN>(acc, a.v[i], b.v[0]);
+    mac<C::CHAIN>(acc, c.v[i], d.v[0]);
     m[i] = ((uint32_t)acc * C::INV) & LMASK;
-    acc += (uint64_t)m[i] * C::MOD[0];
+    mac_k<C::CHAIN>(acc, m[i], C::MOD[0]);
     acc >>= LB;
   }
 #pragma unroll
   for (int i = NL; i < 2 * NL - 1; ++i) {
 #pragma unroll
     for (int j = i - NL + 1; j < NL; ++j) {
-      acc += (uint64_t)a.v[j] * b.v[i - j];
-      acc += (uint64_t)c.v[j] * d.v[i - j];
-      acc += (uint64_t)m[j] * C::MOD[i - j];
+      mac<C::CHAIN>(acc, a.v[j], b.v[i - j]);
+      mac<C::CHAIN>(acc, c.v[j], d.v[i - j]);
+      mac_k<C::CHAIN>(acc, m[j], C::MOD[i - j]);
     }
     r.v[i - NL] = (uint32_t)acc & LMASK;
     acc >>= LB;
@@ -202,29 +235,29 @@ ZDEV Fe<C> mul4(const Fe<C>& a, const Fe<C>& b, const Fe<C>& c, const Fe<C>& d, 
   for (int i = 0; i < NL; ++i) {
 #pragma unroll
     for (int j = 0; j < i; ++j) {
-      acc += (uint64_t)a.v[j] * b.v[i - j];
-      acc += (uint64_t)c.v[j] * d.v[i - j];
-      acc += (uint64_t)e.v[j] * f.v[i - j];
-      acc += (uint64_t)g.v[j] * h.v[i - j];
-      acc += (uint64_t)m[j] * C::MOD[i - j];
+      mac<C::CHAIN>(acc, a.v[j], b.v[i - j]);
+      mac<C::CHAIN>(acc, c.v[j], d.v[i - j]);
+      mac<C::CHAIN>(acc, e.v[j], f.v[i - j]);
+      mac<C::CHAIN>(acc, g.v[j], h.v[i - j]);
+      mac_k<C::CHAIN>(acc, m[j], C::MOD[i - j]);
     }
-    acc += (uint64_t)a.v[i] * b.v[0];
-    acc += (uint64_t)c.v[i] * d.v[0];
-    acc += (uint64_t)e.v[i] * f.v[0];
-    acc += (uint64_t)g.v[i] * h.v[0];
+    mac<C::CHAIN>(acc, a.v[i], b.v[0]);
+    mac<C::CHAIN>(acc, c.v[i], d.v[0]);
+    mac<C::CHAIN>(acc, e.v[i], f.v[0]);
+    mac<C::CHAIN>(acc, g.v[i], h.v[0]);
     m[i] = ((uint32_t)acc * C::INV) & LMASK;
-    acc += (uint64_t)m[i] * C::MOD[0];
+    mac_k<C::CHAIN>(acc, m[i], C::MOD[0]);
     acc >>= LB;
   }
 #pragma unroll
   for (int i = NL; i < 2 * NL - 1; ++i) {
 #pragma unroll
     for (int j = i - NL + 1; j < NL; ++j) {
-      acc += (uint64_t)a.v[j] * b.v[i - j];
-      acc += (uint64_t)c.v[j] * d.v[i - j];
-      acc += (uint64_t)e.v[j] * f.v[i - j];
-      acc += (uint64_t)g.v[j] * h.v[i - j];
-      acc += (uint64_t)m[j] * C::MOD[i - j];
+      mac<C::CHAIN>(acc, a.v[j], b.v[i - j]);
+      mac<C::CHAIN>(acc, c.v[j], d.v[i - j]);
+      mac<C::CHAIN>(acc, e.v[j], f.v[i - j]);
+      mac<C::CHAIN>(acc, g.v[j], h.v[i - j]);
+      mac_k<C::CHAIN>(acc, m[j], C::MOD[i - j]);
     }
     r.v[i - NL] = (uint32_t)acc & LMASK;
     acc >>= LB;
@@ -244,21 +277,21 @@ ZDEV Fe<C> sqr(const Fe<C>& a) {
 #pragma unroll
   for (int i = 0; i < NL; ++i) {
 #pragma unroll
-    for (int j = 0; j < (i + 1) / 2; ++j) acc += (uint64_t)d[j] * a.v[i - j];
-    if ((i & 1) == 0) acc += (uint64_t)a.v[i / 2] * a.v[i / 2];
+    for (int j = 0; j < (i + 1) / 2; ++j) mac<C::CHAIN>(acc, d[j], a.v[i - j]);
+    if ((i & 1) == 0) mac<C::CHAIN>(acc, a.v[i / 2], a.v[i / 2]);
 #pragma unroll
-    for (int j = 0; j < i; ++j) acc += (uint64_t)m[j] * C::MOD[i - j];
+    for (int j = 0; j < i; ++j) mac_k<C::CHAIN>(acc, m[j], C::MOD[i - j]);
     m[i] = ((uint32_t)acc * C::INV) & LMASK;
-    acc += (uint64_t)m[i] * C::MOD[0];
+    mac_k<C::CHAIN>(acc, m[i], C::MOD[0]);
     acc >>= LB;
   }
 #pragma unroll
   for (int i = NL; i < 2 * NL - 1; ++i) {
 #pragma unroll
-    for (int j = i - NL + 1; j < (i + 1) / 2; ++j) acc += (uint64_t)d[j] * a.v[i - j];
-    if ((i & 1) == 0) acc += (uint64_t)a.v[i / 2] * a.v[i / 2];
+    for (int j = i - NL + 1; j < (i + 1) / 2; ++j) mac<C::CHAIN>(acc, d[j], a.v[i - j]);
+    if ((i & 1) == 0) mac<C::CHAIN>(acc, a.v[i / 2], a.v[i / 2]);
 #pragma unroll
-    for (int j = i - NL + 1; j < NL; ++j) acc += (uint64_t)m[j] * C::MOD[i - j];
+    for (int j = i - NL + 1; j < NL; ++j) mac_k<C::CHAIN>(acc, m[j], C::MOD[i - j]);
     r.v[i - NL] = (uint32_t)acc & LMASK;
     acc >>= LB;
   }

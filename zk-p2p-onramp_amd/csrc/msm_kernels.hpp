@@ -125,13 +125,25 @@ ZDEV uint32_t task_len(uint32_t t, const uint32_t* __restrict__ start, const uin
 #define ZKP_ACC_VALS_AHEAD 1
 #endif
 
+// the field the accumulation computes in: G1 with product columns as asm mad chains (consts.hpp
+// FqAccCfg: same values and storage, the 4-wave accumulation hides their wait states), G2 as is
+template <class F>
+struct AccField {
+  using type = F;
+};
+template <>
+struct AccField<Fq> {
+  using type = Fe<FqAccCfg>;
+};
+
 // thread i runs task perm[i] (tasks ordered by length, longest first: the lanes of a wave run
 // equally long chains) or task i (perm == nullptr)
-template <class F>
+template <class FS>
 ZDEV void accumulate(uint32_t i, const uint32_t* __restrict__ points, const uint32_t* __restrict__ vals,
                      const uint32_t* __restrict__ start, const uint32_t* __restrict__ end,
                      const uint32_t* __restrict__ off, uint32_t nb, uint32_t S, const uint32_t* __restrict__ perm,
                      uint32_t* __restrict__ out) {
+  using F = typename AccField<FS>::type;
   if (i >= off[nb]) return;
   const uint32_t t = perm ? perm[i] : i;
   const uint32_t b = seg_search(off, nb, t);

@@ -41,6 +41,7 @@ constexpr int MAX_PASS_BITS = 8;
 constexpr int MAX_TW = ZKP_NTT_MUL2 ? (1 << MAX_PASS_BITS) : (1 << (MAX_PASS_BITS - 1));  // stage roots, b <= 8
 constexpr int RW = ZKP_NTT_SHOUP ? 2 * NL : (ZKP_NTT_PACKED ? 8 : NL);  // LDS words per root
 
+
 __device__ __forceinline__ uint32_t brev(uint32_t x, int b) { return __builtin_bitreverse32(x) >> (32 - b); }
 
 // w_n^E from the two-level table, E < n
@@ -186,70 +187,78 @@ __device__ __forceinline__ Fr stage_sub(const Fr& x, const Fr& y) { return ZKP_N
 __device__ __forceinline__ Fr bfly_d(const Fr& x, const Fr& y, const uint32_t* __restrict__ ltw, uint32_t j) {
   return j ? root_mul(rsub(x, y), ltw, j) : stage_sub(x, y);
 }
-// b radix-2 DIF stages on the LDS tile (rows natural in, bit-reversed out), done two at a
-// time as radix-4 groups in registers (half the LDS traffic and barriers of radix-2):
-// rows r0 + {0, H/2, H, 3H/2} of stage t (span H) and t+1 (span H/2), r0 = grp 2H + i.
+
+// one radix-4 unit (thread work item q) of round t: rows r0 + {0, H/2, H, 3H/2} of stage t
+// (span H) and t+1 (span H/2), r0 = grp 2H + i
 template <int LE>
-__device__ __forceinline__ void dft_stages(uint32_t* __restrict__ lds, const uint32_t* __restrict__ ltw, int E_rt, int b,
-                                           int lc) {
+__device__ __forceinline__ void r4_unit(uint32_t* __restrict__ lds, const uint32_t* __restrict__ ltw, int E, int b,
+                                        int lc, int t, int q) {
+  const uint32_t C = 1u << lc;
+  const int lhalf = b - 1 - t;
+  const uint32_t Hh = 1u << (lhalf - 1);
+  const uint32_t col = (uint32_t)q & (C - 1), bq = ((uint32_t)q >> lc) & ((1u << (b - 2)) - 1);
+  const uint32_t bl = (uint32_t)q >> (lc + b - 2);
+  const uint32_t i = bq & (Hh - 1), grp = bq >> (lhalf - 1);
+  const uint32_t r0 = (grp << (lhalf + 1)) | i;
+  const int base = (int)(bl << (b + lc)) + (int)col;
+  const int st = (int)(Hh << lc);
+  // swizzled rows e0 + k st = e0 | k st (disjoint bits): p0 ^ swz(k st)
+  const int p0 = swz(base + (int)(r0 << lc)), p1 = p0 ^ swz(st), p2 = p0 ^ swz(2 * st), p3 = p0 ^ swz(3 * st);
+  const Fr x0 = lds_get<LE>(lds, E, p0), x1 = lds_get<LE>(lds, E, p1), x2 = lds_get<LE>(lds, E, p2),
+           x3 = lds_get<LE>(lds, E, p3);
+  // stage t: (x0, x2) with w_(2H)^i, (x1, x3) with w_(2H)^(i + H/2); stage t+1: (s02, s13)
+  // and (d02, d13), both with w_H^i.  Roots as exponents of w_(2^b) (stage t: i << t).
+#if ZKP_NTT_MUL2
+  if (Hh > 1) {
+    // y0 = s02 + s13 and y1 = (s02 - s13) w_H^i with the sums raw (< 4m, one reduction);
+    // y2 = d02 + d13 and y3 = (d02 - d13) w_H^i as lazily reduced sums of products over
+    // u = x0 - x2 and v = x1 - x3 with combined roots (r4_dif): 3 reductions per unit, not 4
+    const uint32_t ia = i << t, ib = (i + Hh) << t, ic = (3 * i) << t;
+    const uint32_t id = ((3 * i + 3 * Hh) << t) & ((1u << b) - 1);  // -w^(3i + H/2) = w^(3i + 3H/2)
+    Fr y0, y1, y2, y3;
+    r4_dif(x0, x1, x2, x3, root(ltw, ia), root(ltw, ib), root(ltw, ic), root(ltw, id), root(ltw, i << (t + 1)), y0,
+           y1, y2, y3);
+    lds_put<LE>(lds, E, p0, y0);
+    lds_put<LE>(lds, E, p1, y1);
+    lds_put<LE>(lds, E, p2, y2);
+    lds_put<LE>(lds, E, p3, y3);
+  } else {  // last pair (span 1, i = 0): roots 1 except w_(2H)^(H/2) for (x1, x3)
+    const Fr d02 = sub(x0, x2);
+    const Fr d13 = mul(rsub(x1, x3), root(ltw, Hh << t));
+    const Fr s02 = add(x0, x2), s13 = add(x1, x3);
+    lds_put<LE>(lds, E, p0, add(s02, s13));
+    lds_put<LE>(lds, E, p1, sub(s02, s13));
+    lds_put<LE>(lds, E, p2, add(d02, d13));
+    lds_put<LE>(lds, E, p3, sub(d02, d13));
+  }
+#else
+  const Fr d02 = bfly_d(x0, x2, ltw, i << t);
+  const Fr d13 = bfly_d(x1, x3, ltw, (i + Hh) << t);
+  const uint32_t j = i << (t + 1);
+  if (Hh > 1) {  // the sums stay raw (< 4m) and meet one reduction; w_H^0 = 1 (Montgomery) for i = 0
+    const Fr s02 = add_raw(x0, x2), s13 = add_raw(x1, x3);
+    lds_put<LE>(lds, E, p0, add_raw_reduce(s02, s13));
+    lds_put<LE>(lds, E, p1, root_mul(sub_raw6(s02, s13), ltw, j));
+  } else {  // last pair (span 1): no multiply in stage t+1
+    const Fr s02 = add(x0, x2), s13 = add(x1, x3);
+    lds_put<LE>(lds, E, p0, add(s02, s13));
+    lds_put<LE>(lds, E, p1, sub(s02, s13));
+  }
+  lds_put<LE>(lds, E, p2, add(d02, d13));
+  lds_put<LE>(lds, E, p3, bfly_d(d02, d13, ltw, j));
+#endif
+}
+
+// b radix-2 DIF stages on the LDS tile (rows natural in, bit-reversed out), done two at a
+// time as radix-4 groups in registers (half the LDS traffic and barriers of radix-2)
+template <int LE>
+__device__ __forceinline__ void dft_stages(uint32_t* __restrict__ lds, const uint32_t* __restrict__ ltw, int E_rt,
+                                           int b, int lc) {
   const int E = LE ? (1 << LE) : E_rt;
   const uint32_t C = 1u << lc;
   int t = 0;
   for (; t + 1 < b; t += 2) {
-    const int lhalf = b - 1 - t;
-    const uint32_t Hh = 1u << (lhalf - 1);
-    for (int q = threadIdx.x; q < (E >> 2); q += TPB) {
-      const uint32_t col = (uint32_t)q & (C - 1), bq = ((uint32_t)q >> lc) & ((1u << (b - 2)) - 1);
-      const uint32_t bl = (uint32_t)q >> (lc + b - 2);
-      const uint32_t i = bq & (Hh - 1), grp = bq >> (lhalf - 1);
-      const uint32_t r0 = (grp << (lhalf + 1)) | i;
-      const int base = (int)(bl << (b + lc)) + (int)col;
-      const int st = (int)(Hh << lc);
-      // swizzled rows e0 + k st = e0 | k st (disjoint bits): p0 ^ swz(k st)
-      const int p0 = swz(base + (int)(r0 << lc)), p1 = p0 ^ swz(st), p2 = p0 ^ swz(2 * st), p3 = p0 ^ swz(3 * st);
-      const Fr x0 = lds_get<LE>(lds, E, p0), x1 = lds_get<LE>(lds, E, p1), x2 = lds_get<LE>(lds, E, p2), x3 = lds_get<LE>(lds, E, p3);
-      // stage t: (x0, x2) with w_(2H)^i, (x1, x3) with w_(2H)^(i + H/2); stage t+1: (s02, s13)
-      // and (d02, d13), both with w_H^i.  Roots as exponents of w_(2^b) (stage t: i << t).
-#if ZKP_NTT_MUL2
-      if (Hh > 1) {
-        // y0 = s02 + s13 and y1 = (s02 - s13) w_H^i with the sums raw (< 4m, one reduction);
-        // y2 = d02 + d13 and y3 = (d02 - d13) w_H^i as lazily reduced sums of products over
-        // u = x0 - x2 and v = x1 - x3 with combined roots (r4_dif): 3 reductions per unit, not 4
-        const uint32_t ia = i << t, ib = (i + Hh) << t, ic = (3 * i) << t;
-        const uint32_t id = ((3 * i + 3 * Hh) << t) & ((1u << b) - 1);  // -w^(3i + H/2) = w^(3i + 3H/2)
-        Fr y0, y1, y2, y3;
-        r4_dif(x0, x1, x2, x3, root(ltw, ia), root(ltw, ib), root(ltw, ic), root(ltw, id), root(ltw, i << (t + 1)),
-               y0, y1, y2, y3);
-        lds_put<LE>(lds, E, p0, y0);
-        lds_put<LE>(lds, E, p1, y1);
-        lds_put<LE>(lds, E, p2, y2);
-        lds_put<LE>(lds, E, p3, y3);
-      } else {  // last pair (span 1, i = 0): roots 1 except w_(2H)^(H/2) for (x1, x3)
-        const Fr d02 = sub(x0, x2);
-        const Fr d13 = mul(rsub(x1, x3), root(ltw, Hh << t));
-        const Fr s02 = add(x0, x2), s13 = add(x1, x3);
-        lds_put<LE>(lds, E, p0, add(s02, s13));
-        lds_put<LE>(lds, E, p1, sub(s02, s13));
-        lds_put<LE>(lds, E, p2, add(d02, d13));
-        lds_put<LE>(lds, E, p3, sub(d02, d13));
-      }
-#else
-      const Fr d02 = bfly_d(x0, x2, ltw, i << t);
-      const Fr d13 = bfly_d(x1, x3, ltw, (i + Hh) << t);
-      const uint32_t j = i << (t + 1);
-      if (Hh > 1) {  // the sums stay raw (< 4m) and meet one reduction; w_H^0 = 1 (Montgomery) for i = 0
-        const Fr s02 = add_raw(x0, x2), s13 = add_raw(x1, x3);
-        lds_put<LE>(lds, E, p0, add_raw_reduce(s02, s13));
-        lds_put<LE>(lds, E, p1, root_mul(sub_raw6(s02, s13), ltw, j));
-      } else {  // last pair (span 1): no multiply in stage t+1
-        const Fr s02 = add(x0, x2), s13 = add(x1, x3);
-        lds_put<LE>(lds, E, p0, add(s02, s13));
-        lds_put<LE>(lds, E, p1, sub(s02, s13));
-      }
-      lds_put<LE>(lds, E, p2, add(d02, d13));
-      lds_put<LE>(lds, E, p3, bfly_d(d02, d13, ltw, j));
-#endif
-    }
+    for (int q = threadIdx.x; q < (E >> 2); q += TPB) r4_unit<LE>(lds, ltw, E, b, lc, t, q);
     __syncthreads();
   }
   if (t < b) {  // odd b: the last radix-2 stage (span 1)
