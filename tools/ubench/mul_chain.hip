@@ -63,6 +63,41 @@ __device__ __forceinline__ void macs(uint64_t& acc, uint32_t x, uint32_t ys) {  
   asm("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc), "=s"(cc) : "v"(x), "s"(ys));
 }
 
+// the same chain from C: after every product the accumulator passes through an EMPTY asm that
+// claims to modify it, so the compiler cannot re-associate the column, but it still sees (and
+// schedules, and hazard-checks) real v_mad_u64_u32 instructions
+__device__ __forceinline__ void macb(uint64_t& acc, uint32_t x, uint32_t y) {
+  acc += (uint64_t)x * y;
+  asm("" : "+v"(acc));
+}
+__device__ __forceinline__ void mul_bar(uint32_t* r, const uint32_t* a, const uint32_t* b) {
+  uint32_t m[9];
+  uint64_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+#pragma unroll
+    for (int j = 0; j < i; ++j) {
+      macb(acc, a[j], b[i - j]);
+      macb(acc, m[j], P29[i - j]);
+    }
+    macb(acc, a[i], b[0]);
+    m[i] = ((uint32_t)acc * PINV) & MASK;
+    macb(acc, m[i], P29[0]);
+    acc >>= 29;
+  }
+#pragma unroll
+  for (int i = 9; i < 17; ++i) {
+#pragma unroll
+    for (int j = i - 8; j < 9; ++j) {
+      macb(acc, a[j], b[i - j]);
+      macb(acc, m[j], P29[i - j]);
+    }
+    r[i - 9] = (uint32_t)acc & MASK;
+    acc >>= 29;
+  }
+  r[8] = (uint32_t)acc;
+}
+
 __device__ __forceinline__ void mul_asm(uint32_t* r, const uint32_t* a, const uint32_t* b) {
   uint32_t m[9];
   uint64_t acc = 0;
@@ -211,6 +246,10 @@ __global__ void k_mul(uint64_t* out, uint32_t seed) {
     } else if (V == 2) {
       mul_asm2(x, x, y, z, z, y);
       mul_asm(w, w, y);
+    } else if (V == 4) {
+      mul_bar(x, x, y);
+      mul_bar(z, z, y);
+      mul_bar(w, w, y);
     } else {
       mul_asm3(x, x, y, z, z, w, w);
     }
@@ -269,8 +308,12 @@ int main() {
     CHK(hipMemcpy(h1, d1, (size_t)cus * bm * 256 * 8, hipMemcpyDeviceToHost));
     size_t bad3 = 0;
     for (size_t i = 0; i < (size_t)cus * bm * 256; ++i) bad3 += h0[i] != h1[i];
+    if (run<4>("fips29_c_barrier_chain", d1, cus * bm, 256, &g)) return 1;
+    CHK(hipMemcpy(h1, d1, (size_t)cus * bm * 256 * 8, hipMemcpyDeviceToHost));
+    size_t bad4 = 0;
+    for (size_t i = 0; i < (size_t)cus * bm * 256; ++i) bad4 += h0[i] != h1[i];
     printf("{\"check\": \"asm == c\", \"blocks\": %d, \"mismatch_chain\": %zu, \"mismatch_x2\": %zu, "
-           "\"mismatch_x3\": %zu}\n", cus * bm, bad, bad2, bad3);
+           "\"mismatch_x3\": %zu, \"mismatch_barrier\": %zu}\n", cus * bm, bad, bad2, bad3, bad4);
     delete[] h0;
     delete[] h1;
   }

@@ -37,38 +37,45 @@ using Fr = Fe<FrCfg>;
 
 #define ZDEV __host__ __device__ __forceinline__
 
-// acc += x * y.  CH (C::CHAIN, device code): one v_mad_u64_u32 in inline assembly, so every product
-// column stays ONE dependent chain seeded by the previous column's carry.  Left to itself the
-// compiler re-associates each column into a sum from 0 plus a 64-bit join of the carry
-// (v_lshl_add_u64 per column); the chain form drops the joins, and the wait states between
-// dependent 64-bit mads (filled with s_nop) cost no VALU issue slot when other waves are ready:
-// 172 -> 183 G products/s at high occupancy (tools/ubench/mul_chain.hip, profiles/mul_chain_r03.txt),
-// slower where few waves hide them.  mac_k takes a constant (an SGPR operand).  ZKP_ASM_MAC=0
-// disables the assembly everywhere; host code is always plain C.
-#ifndef ZKP_ASM_MAC
-#define ZKP_ASM_MAC 1
+// acc += x * y.  CH (C::CHAIN, device code): every product column stays ONE dependent chain seeded
+// by the previous column's carry.  Left to itself the compiler re-associates each column into a sum
+// from 0 plus a 64-bit join of the carry (v_lshl_add_u64 per column).  ZKP_MAC_FORM 2 (default):
+// after each product the accumulator passes through an EMPTY asm statement that claims to modify
+// it, so the column cannot be re-associated while the compiler still sees, schedules and
+// hazard-checks real v_mad_u64_u32 instructions (it interleaves independent products' chains to
+// cover the wait states between dependent 64-bit mads); 1: the mad itself as inline asm (the
+// compiler then pads every one with s_nop); 0: no chains.  tools/ubench/mul_chain.hip,
+// profiles/mul_chain_r03.txt.  mac_k takes a constant.  Host code is always plain C.
+#ifndef ZKP_MAC_FORM
+#define ZKP_MAC_FORM 2
 #endif
 template <bool CH>
 ZDEV void mac(uint64_t& acc, uint32_t x, uint32_t y) {
-#if ZKP_ASM_MAC && defined(__HIP_DEVICE_COMPILE__)
-  if constexpr (CH) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (CH && ZKP_MAC_FORM == 1) {
     uint64_t cc;
     asm("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc), "=s"(cc) : "v"(x), "v"(y));
     return;
   }
 #endif
   acc += (uint64_t)x * y;
+#if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (CH && ZKP_MAC_FORM == 2) asm("" : "+v"(acc));
+#endif
 }
 template <bool CH>
 ZDEV void mac_k(uint64_t& acc, uint32_t x, uint32_t k) {
-#if ZKP_ASM_MAC && defined(__HIP_DEVICE_COMPILE__)
-  if constexpr (CH) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (CH && ZKP_MAC_FORM == 1) {
     uint64_t cc;
     asm("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc), "=s"(cc) : "v"(x), "s"(k));
     return;
   }
 #endif
   acc += (uint64_t)x * k;
+#if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (CH && ZKP_MAC_FORM == 2) asm("" : "+v"(acc));
+#endif
 }
 
 template <class C>
