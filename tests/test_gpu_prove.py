@@ -191,6 +191,38 @@ def test_concurrent_prove_on_one_handle(golden_dir):
     assert not errs and got == want
 
 
+def test_staged_concurrent_on_inflight_pipelines(golden_dir, monkeypatch):
+    """ZKP_INFLIGHT=2: staged witnesses live in device 0's first pipeline; two host threads
+    calling zkp_prove_staged at once take both pipelines (the second reads the witness in place).
+    Every concurrent proof equals the golden proof."""
+    import threading
+    monkeypatch.setenv("ZKP_INFLIGHT", "2")
+    zk, wt = _files(golden_dir, "venmo_mini")
+    man = json.load(open(os.path.join(golden_dir, "manifest.json")))["circuits"]["venmo_mini"]
+    r, s = int(man["r"]), int(man["s"])
+    want = open(os.path.join(golden_dir, "proof_venmo_mini.json")).read()
+    p = zkp_amd.Prover(zk)
+    for slot in range(2):
+        p.stage(wt, slot=slot)
+    ref = p.prove_staged_raw(0, r, s)
+    assert groth16.js_stringify(zkp_amd.proof_object(*ref[0])) == want
+    out, errs = [], []
+
+    def work(k):
+        try:
+            for i in range(6):
+                out.append(p.prove_staged_raw((i + k) % 2, r, s))
+        except BaseException as e:  # re-raised below
+            errs.append(e)
+    th = [threading.Thread(target=work, args=(k,)) for k in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs, errs
+    assert len(out) == 12 and all(o == ref for o in out)
+
+
 @pytest.mark.parametrize("circuit", ["small", "venmo_mini"])
 def test_batch_inflight_shared_tables(golden_dir, monkeypatch, circuit):
     """ZKP_INFLIGHT=3: three pipelines on device 0 share one copy of the base tables; a batch
