@@ -74,6 +74,40 @@ template <class C>
 ZDEV Fe<C> acc_xcanon(const Fe<C>& x) { return canon8(x); }
 ZDEV Fq2 acc_xcanon(const Fq2& x) { return canon4(x); }
 
+// independent pairs of products (ZKP_MUL_PAIRS, default on): a chained field config (C::CHAIN) runs
+// each pair in lockstep (field.hpp mul_pair / sqr_pair); otherwise, and for Fq2, two plain products
+#ifndef ZKP_MUL_PAIRS
+#define ZKP_MUL_PAIRS 1
+#endif
+template <class F>
+ZDEV void mul_2(const F& a, const F& b, const F& c, const F& d, F& r, F& s) {
+  r = mul(a, b);
+  s = mul(c, d);
+}
+template <class C>
+ZDEV void mul_2(const Fe<C>& a, const Fe<C>& b, const Fe<C>& c, const Fe<C>& d, Fe<C>& r, Fe<C>& s) {
+  if constexpr (C::CHAIN && ZKP_MUL_PAIRS) {
+    mul_pair(a, b, c, d, r, s);
+  } else {
+    r = mul(a, b);
+    s = mul(c, d);
+  }
+}
+template <class F>
+ZDEV void acc_sqr_2(const F& a, const F& c, F& r, F& s) {
+  r = acc_sqr(a);
+  s = acc_sqr(c);
+}
+template <class C>
+ZDEV void acc_sqr_2(const Fe<C>& a, const Fe<C>& c, Fe<C>& r, Fe<C>& s) {
+  if constexpr (C::CHAIN && ZKP_MUL_PAIRS) {
+    sqr_pair(a, c, r, s);
+  } else {
+    r = acc_sqr(a);
+    s = acc_sqr(c);
+  }
+}
+
 template <class F>
 ZDEV Xyzz<F> xyzz_inf() {
   Xyzz<F> r;
@@ -150,12 +184,12 @@ ZDEV void xyzz_add_aff(Xyzz<F>& acc, const Aff<F>& q, bool neg = false) {
     return;
   }
   const F qy = neg ? rsub(f_zero<F>(), q.y) : q.y;  // mul operand only
-  F U2 = mul(q.x, acc.zz);
-  F S2 = mul(qy, acc.zzz);
+  F U2, S2;
+  mul_2(q.x, acc.zz, qy, acc.zzz, U2, S2);
   F P = acc_xsub(U2, acc.x);
   F R = acc_sub(S2, acc.y);
-  F PP = acc_sqr(P);
-  F RR = acc_sqr(R);
+  F PP, RR;
+  acc_sqr_2(P, R, PP, RR);
   if (is_zero(PP)) {
     if (is_zero(RR)) {
       Aff<F> qs = q;
@@ -166,12 +200,14 @@ ZDEV void xyzz_add_aff(Xyzz<F>& acc, const Aff<F>& q, bool neg = false) {
     }
     return;
   }
-  F PPP = mul(P, PP);
-  F Q = mul(acc.x, PP);
+  F PPP, Q;
+  mul_2(P, PP, acc.x, PP, PPP, Q);
   F X3 = acc_x3(RR, PPP, Q);
   F Y3 = acc_y3(R, acc_xsub(Q, X3), acc.y, acc_negd(PPP));  // R (Q - X3) - Y1 PPP
-  acc.zz = mul(acc.zz, PP);
-  acc.zzz = mul(acc.zzz, PPP);
+  F ZZ3, ZZZ3;
+  mul_2(acc.zz, PP, acc.zzz, PPP, ZZ3, ZZZ3);
+  acc.zz = ZZ3;
+  acc.zzz = ZZZ3;
   acc.x = X3;
   acc.y = Y3;
 }

@@ -306,6 +306,106 @@ ZDEV Fe<C> sqr(const Fe<C>& a) {
   return r;
 }
 
+// Two independent Montgomery products / squares in lockstep (the chained columns of both
+// interleave, so a dependent mad of one chain follows an independent mad of the other instead of
+// a wait state).  Same arithmetic as mul() / sqr() on each pair.
+template <class C>
+ZDEV void mul_pair(const Fe<C>& a, const Fe<C>& b, const Fe<C>& c, const Fe<C>& d, Fe<C>& r, Fe<C>& s) {
+  uint32_t m[NL], n[NL];
+  uint64_t x = 0, y = 0;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) {
+#pragma unroll
+    for (int j = 0; j < i; ++j) {
+      mac<C::CHAIN>(x, a.v[j], b.v[i - j]);
+      mac<C::CHAIN>(y, c.v[j], d.v[i - j]);
+      mac_k<C::CHAIN>(x, m[j], C::MOD[i - j]);
+      mac_k<C::CHAIN>(y, n[j], C::MOD[i - j]);
+    }
+    mac<C::CHAIN>(x, a.v[i], b.v[0]);
+    mac<C::CHAIN>(y, c.v[i], d.v[0]);
+    m[i] = ((uint32_t)x * C::INV) & LMASK;
+    n[i] = ((uint32_t)y * C::INV) & LMASK;
+    mac_k<C::CHAIN>(x, m[i], C::MOD[0]);
+    mac_k<C::CHAIN>(y, n[i], C::MOD[0]);
+    x >>= LB;
+    y >>= LB;
+  }
+#pragma unroll
+  for (int i = NL; i < 2 * NL - 1; ++i) {
+#pragma unroll
+    for (int j = i - NL + 1; j < NL; ++j) {
+      mac<C::CHAIN>(x, a.v[j], b.v[i - j]);
+      mac<C::CHAIN>(y, c.v[j], d.v[i - j]);
+      mac_k<C::CHAIN>(x, m[j], C::MOD[i - j]);
+      mac_k<C::CHAIN>(y, n[j], C::MOD[i - j]);
+    }
+    r.v[i - NL] = (uint32_t)x & LMASK;
+    s.v[i - NL] = (uint32_t)y & LMASK;
+    x >>= LB;
+    y >>= LB;
+  }
+  r.v[NL - 1] = (uint32_t)x;
+  s.v[NL - 1] = (uint32_t)y;
+}
+
+template <class C>
+ZDEV void sqr_pair(const Fe<C>& a, const Fe<C>& c, Fe<C>& r, Fe<C>& s) {
+  uint32_t m[NL], n[NL], da[NL], dc[NL];
+#pragma unroll
+  for (int i = 0; i < NL; ++i) {
+    da[i] = a.v[i] << 1;
+    dc[i] = c.v[i] << 1;
+  }
+  uint64_t x = 0, y = 0;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) {
+#pragma unroll
+    for (int j = 0; j < (i + 1) / 2; ++j) {
+      mac<C::CHAIN>(x, da[j], a.v[i - j]);
+      mac<C::CHAIN>(y, dc[j], c.v[i - j]);
+    }
+    if ((i & 1) == 0) {
+      mac<C::CHAIN>(x, a.v[i / 2], a.v[i / 2]);
+      mac<C::CHAIN>(y, c.v[i / 2], c.v[i / 2]);
+    }
+#pragma unroll
+    for (int j = 0; j < i; ++j) {
+      mac_k<C::CHAIN>(x, m[j], C::MOD[i - j]);
+      mac_k<C::CHAIN>(y, n[j], C::MOD[i - j]);
+    }
+    m[i] = ((uint32_t)x * C::INV) & LMASK;
+    n[i] = ((uint32_t)y * C::INV) & LMASK;
+    mac_k<C::CHAIN>(x, m[i], C::MOD[0]);
+    mac_k<C::CHAIN>(y, n[i], C::MOD[0]);
+    x >>= LB;
+    y >>= LB;
+  }
+#pragma unroll
+  for (int i = NL; i < 2 * NL - 1; ++i) {
+#pragma unroll
+    for (int j = i - NL + 1; j < (i + 1) / 2; ++j) {
+      mac<C::CHAIN>(x, da[j], a.v[i - j]);
+      mac<C::CHAIN>(y, dc[j], c.v[i - j]);
+    }
+    if ((i & 1) == 0) {
+      mac<C::CHAIN>(x, a.v[i / 2], a.v[i / 2]);
+      mac<C::CHAIN>(y, c.v[i / 2], c.v[i / 2]);
+    }
+#pragma unroll
+    for (int j = i - NL + 1; j < NL; ++j) {
+      mac_k<C::CHAIN>(x, m[j], C::MOD[i - j]);
+      mac_k<C::CHAIN>(y, n[j], C::MOD[i - j]);
+    }
+    r.v[i - NL] = (uint32_t)x & LMASK;
+    s.v[i - NL] = (uint32_t)y & LMASK;
+    x >>= LB;
+    y >>= LB;
+  }
+  r.v[NL - 1] = (uint32_t)x;
+  s.v[NL - 1] = (uint32_t)y;
+}
+
 // carry-propagate limbs 0..7 into 29-bit digits (limb values must be >= 0 and < 2^31)
 template <class C>
 ZDEV void normalize(Fe<C>& a) {
