@@ -98,6 +98,37 @@ __device__ __forceinline__ void mul_bar(uint32_t* r, const uint32_t* a, const ui
   r[8] = (uint32_t)acc;
 }
 
+// the barrier only on the carry at each column start (acc >>= 29): one empty asm per column
+__device__ __forceinline__ void mul_cbar(uint32_t* r, const uint32_t* a, const uint32_t* b) {
+  uint32_t m[9];
+  uint64_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+#pragma unroll
+    for (int j = 0; j < i; ++j) {
+      acc += (uint64_t)a[j] * b[i - j];
+      acc += (uint64_t)m[j] * P29[i - j];
+    }
+    acc += (uint64_t)a[i] * b[0];
+    m[i] = ((uint32_t)acc * PINV) & MASK;
+    acc += (uint64_t)m[i] * P29[0];
+    acc >>= 29;
+    asm("" : "+v"(acc));
+  }
+#pragma unroll
+  for (int i = 9; i < 17; ++i) {
+#pragma unroll
+    for (int j = i - 8; j < 9; ++j) {
+      acc += (uint64_t)a[j] * b[i - j];
+      acc += (uint64_t)m[j] * P29[i - j];
+    }
+    r[i - 9] = (uint32_t)acc & MASK;
+    acc >>= 29;
+    asm("" : "+v"(acc));
+  }
+  r[8] = (uint32_t)acc;
+}
+
 __device__ __forceinline__ void mul_asm(uint32_t* r, const uint32_t* a, const uint32_t* b) {
   uint32_t m[9];
   uint64_t acc = 0;
@@ -250,6 +281,10 @@ __global__ void k_mul(uint64_t* out, uint32_t seed) {
       mul_bar(x, x, y);
       mul_bar(z, z, y);
       mul_bar(w, w, y);
+    } else if (V == 5) {
+      mul_cbar(x, x, y);
+      mul_cbar(z, z, y);
+      mul_cbar(w, w, y);
     } else {
       mul_asm3(x, x, y, z, z, w, w);
     }
@@ -312,8 +347,13 @@ int main() {
     CHK(hipMemcpy(h1, d1, (size_t)cus * bm * 256 * 8, hipMemcpyDeviceToHost));
     size_t bad4 = 0;
     for (size_t i = 0; i < (size_t)cus * bm * 256; ++i) bad4 += h0[i] != h1[i];
+    if (run<5>("fips29_c_carry_barrier", d1, cus * bm, 256, &g)) return 1;
+    CHK(hipMemcpy(h1, d1, (size_t)cus * bm * 256 * 8, hipMemcpyDeviceToHost));
+    size_t bad5 = 0;
+    for (size_t i = 0; i < (size_t)cus * bm * 256; ++i) bad5 += h0[i] != h1[i];
     printf("{\"check\": \"asm == c\", \"blocks\": %d, \"mismatch_chain\": %zu, \"mismatch_x2\": %zu, "
-           "\"mismatch_x3\": %zu, \"mismatch_barrier\": %zu}\n", cus * bm, bad, bad2, bad3, bad4);
+           "\"mismatch_x3\": %zu, \"mismatch_barrier\": %zu, \"mismatch_carry_barrier\": %zu}\n", cus * bm, bad, bad2,
+           bad3, bad4, bad5);
     delete[] h0;
     delete[] h1;
   }

@@ -349,6 +349,104 @@ ZDEV void mul_pair(const Fe<C>& a, const Fe<C>& b, const Fe<C>& c, const Fe<C>& 
   s.v[NL - 1] = (uint32_t)y;
 }
 
+// three independent products in lockstep (two other mads between dependent ones of a chain)
+template <class C>
+ZDEV void mul_triple(const Fe<C>& a, const Fe<C>& b, const Fe<C>& c, const Fe<C>& d, const Fe<C>& e, const Fe<C>& f,
+                     Fe<C>& r, Fe<C>& s, Fe<C>& t) {
+  uint32_t m[NL], n[NL], o[NL];
+  uint64_t x = 0, y = 0, z = 0;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) {
+#pragma unroll
+    for (int j = 0; j < i; ++j) {
+      mac<C::CHAIN>(x, a.v[j], b.v[i - j]);
+      mac<C::CHAIN>(y, c.v[j], d.v[i - j]);
+      mac<C::CHAIN>(z, e.v[j], f.v[i - j]);
+      mac_k<C::CHAIN>(x, m[j], C::MOD[i - j]);
+      mac_k<C::CHAIN>(y, n[j], C::MOD[i - j]);
+      mac_k<C::CHAIN>(z, o[j], C::MOD[i - j]);
+    }
+    mac<C::CHAIN>(x, a.v[i], b.v[0]);
+    mac<C::CHAIN>(y, c.v[i], d.v[0]);
+    mac<C::CHAIN>(z, e.v[i], f.v[0]);
+    m[i] = ((uint32_t)x * C::INV) & LMASK;
+    n[i] = ((uint32_t)y * C::INV) & LMASK;
+    o[i] = ((uint32_t)z * C::INV) & LMASK;
+    mac_k<C::CHAIN>(x, m[i], C::MOD[0]);
+    mac_k<C::CHAIN>(y, n[i], C::MOD[0]);
+    mac_k<C::CHAIN>(z, o[i], C::MOD[0]);
+    x >>= LB;
+    y >>= LB;
+    z >>= LB;
+  }
+#pragma unroll
+  for (int i = NL; i < 2 * NL - 1; ++i) {
+#pragma unroll
+    for (int j = i - NL + 1; j < NL; ++j) {
+      mac<C::CHAIN>(x, a.v[j], b.v[i - j]);
+      mac<C::CHAIN>(y, c.v[j], d.v[i - j]);
+      mac<C::CHAIN>(z, e.v[j], f.v[i - j]);
+      mac_k<C::CHAIN>(x, m[j], C::MOD[i - j]);
+      mac_k<C::CHAIN>(y, n[j], C::MOD[i - j]);
+      mac_k<C::CHAIN>(z, o[j], C::MOD[i - j]);
+    }
+    r.v[i - NL] = (uint32_t)x & LMASK;
+    s.v[i - NL] = (uint32_t)y & LMASK;
+    t.v[i - NL] = (uint32_t)z & LMASK;
+    x >>= LB;
+    y >>= LB;
+    z >>= LB;
+  }
+  r.v[NL - 1] = (uint32_t)x;
+  s.v[NL - 1] = (uint32_t)y;
+  t.v[NL - 1] = (uint32_t)z;
+}
+
+// a product and a lazily reduced sum of two products (mul2) in lockstep
+template <class C>
+ZDEV void mul_mul2_pair(const Fe<C>& a, const Fe<C>& b, const Fe<C>& c, const Fe<C>& d, const Fe<C>& e,
+                        const Fe<C>& f, Fe<C>& r, Fe<C>& s) {
+  uint32_t m[NL], n[NL];
+  uint64_t x = 0, y = 0;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) {
+#pragma unroll
+    for (int j = 0; j < i; ++j) {
+      mac<C::CHAIN>(y, c.v[j], d.v[i - j]);
+      mac<C::CHAIN>(x, a.v[j], b.v[i - j]);
+      mac<C::CHAIN>(y, e.v[j], f.v[i - j]);
+      mac_k<C::CHAIN>(x, m[j], C::MOD[i - j]);
+      mac_k<C::CHAIN>(y, n[j], C::MOD[i - j]);
+    }
+    mac<C::CHAIN>(y, c.v[i], d.v[0]);
+    mac<C::CHAIN>(x, a.v[i], b.v[0]);
+    mac<C::CHAIN>(y, e.v[i], f.v[0]);
+    m[i] = ((uint32_t)x * C::INV) & LMASK;
+    n[i] = ((uint32_t)y * C::INV) & LMASK;
+    mac_k<C::CHAIN>(x, m[i], C::MOD[0]);
+    mac_k<C::CHAIN>(y, n[i], C::MOD[0]);
+    x >>= LB;
+    y >>= LB;
+  }
+#pragma unroll
+  for (int i = NL; i < 2 * NL - 1; ++i) {
+#pragma unroll
+    for (int j = i - NL + 1; j < NL; ++j) {
+      mac<C::CHAIN>(y, c.v[j], d.v[i - j]);
+      mac<C::CHAIN>(x, a.v[j], b.v[i - j]);
+      mac<C::CHAIN>(y, e.v[j], f.v[i - j]);
+      mac_k<C::CHAIN>(x, m[j], C::MOD[i - j]);
+      mac_k<C::CHAIN>(y, n[j], C::MOD[i - j]);
+    }
+    r.v[i - NL] = (uint32_t)x & LMASK;
+    s.v[i - NL] = (uint32_t)y & LMASK;
+    x >>= LB;
+    y >>= LB;
+  }
+  r.v[NL - 1] = (uint32_t)x;
+  s.v[NL - 1] = (uint32_t)y;
+}
+
 template <class C>
 ZDEV void sqr_pair(const Fe<C>& a, const Fe<C>& c, Fe<C>& r, Fe<C>& s) {
   uint32_t m[NL], n[NL], da[NL], dc[NL];
