@@ -165,6 +165,46 @@ ZDEV Fe<C> mul_shoup(const Fe<C>& a, const Fe<C>& w, const Fe<C>& wq) {
   return r;
 }
 
+// two independent Shoup products a w, c v in lockstep (column chains interleaved, as mul_pair)
+template <class C>
+ZDEV void mul_shoup_pair(const Fe<C>& a, const Fe<C>& w, const Fe<C>& wq, const Fe<C>& c, const Fe<C>& v,
+                         const Fe<C>& vq, Fe<C>& r, Fe<C>& s) {
+  uint32_t q[NL], p[NL];
+  uint64_t x = 0, y = 0;
+#pragma unroll
+  for (int k = 7; k < 2 * NL - 1; ++k) {
+#pragma unroll
+    for (int i = (k - NL + 1 > 0 ? k - NL + 1 : 0); i <= (k < NL - 1 ? k : NL - 1); ++i) {
+      mac<C::CHAIN>(x, a.v[i], wq.v[k - i]);
+      mac<C::CHAIN>(y, c.v[i], vq.v[k - i]);
+    }
+    if (k >= NL) {
+      q[k - NL] = (uint32_t)x & LMASK;
+      p[k - NL] = (uint32_t)y & LMASK;
+    }
+    x >>= LB;
+    y >>= LB;
+  }
+  q[NL - 1] = (uint32_t)x;
+  p[NL - 1] = (uint32_t)y;
+  x = 0;
+  y = 0;
+#pragma unroll
+  for (int k = 0; k < NL; ++k) {
+#pragma unroll
+    for (int i = 0; i <= k; ++i) {
+      mac<C::CHAIN>(x, a.v[i], w.v[k - i]);
+      mac<C::CHAIN>(y, c.v[i], v.v[k - i]);
+      mac_k<C::CHAIN>(x, q[i], C::NM[k - i]);
+      mac_k<C::CHAIN>(y, p[i], C::NM[k - i]);
+    }
+    r.v[k] = (uint32_t)x & LMASK;
+    s.v[k] = (uint32_t)y & LMASK;
+    x >>= LB;
+    y >>= LB;
+  }
+}
+
 // Shoup quotient of a constant from its canonical Montgomery form wm = w 2^261 mod m (< m):
 // w 2^261 = wq m + wm, so wq = floor(w 2^261 / m) = -wm m^-1 mod 2^261 (a low-half product).
 template <class C>

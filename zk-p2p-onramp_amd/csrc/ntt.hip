@@ -187,6 +187,27 @@ __device__ __forceinline__ Fr stage_sub(const Fr& x, const Fr& y) { return ZKP_N
 __device__ __forceinline__ Fr bfly_d(const Fr& x, const Fr& y, const uint32_t* __restrict__ ltw, uint32_t j) {
   return j ? root_mul(rsub(x, y), ltw, j) : stage_sub(x, y);
 }
+// ZKP_NTT_PAIRS (Shoup builds, default on): a * w_ja and c * w_jc as one lockstep pair of Shoup
+// products (field.hpp mul_shoup_pair; with Fr's chained columns the two chains fill each other's
+// wait states); outputs < 3m
+#ifndef ZKP_NTT_PAIRS
+#define ZKP_NTT_PAIRS ZKP_NTT_SHOUP
+#endif
+#if ZKP_NTT_PAIRS && (!ZKP_NTT_SHOUP || ZKP_NTT_MUL2)
+#error "ZKP_NTT_PAIRS needs the Shoup four-multiply unit"
+#endif
+__device__ __forceinline__ void root_mul_pair(const Fr& a, uint32_t ja, const Fr& c, uint32_t jc,
+                                              const uint32_t* __restrict__ ltw, Fr& r, Fr& s) {
+  Fr w, wq, v, vq;
+#pragma unroll
+  for (int l = 0; l < NL; ++l) {
+    w.v[l] = ltw[l * MAX_TW + ja];
+    wq.v[l] = ltw[(NL + l) * MAX_TW + ja];
+    v.v[l] = ltw[l * MAX_TW + jc];
+    vq.v[l] = ltw[(NL + l) * MAX_TW + jc];
+  }
+  mul_shoup_pair(a, w, wq, c, v, vq, r, s);
+}
 
 // one radix-4 unit (thread work item q) of round t: rows r0 + {0, H/2, H, 3H/2} of stage t
 // (span H) and t+1 (span H/2), r0 = grp 2H + i
@@ -232,6 +253,27 @@ __device__ __forceinline__ void r4_unit(uint32_t* __restrict__ lds, const uint32
     lds_put<LE>(lds, E, p3, sub(d02, d13));
   }
 #else
+#if ZKP_NTT_PAIRS
+  // the unit's independent root products in lockstep pairs (d02 / d13, then y1 / y3 by the same
+  // root); every lane multiplies (w^0 = 1 for i = 0: no divergent j == 0 path)
+  const uint32_t j = i << (t + 1);
+  Fr d02, d13;
+  root_mul_pair(rsub(x0, x2), i << t, rsub(x1, x3), (i + Hh) << t, ltw, d02, d13);
+  if (Hh > 1) {  // the sums stay raw (< 4m) and meet one reduction
+    const Fr s02 = add_raw(x0, x2), s13 = add_raw(x1, x3);
+    lds_put<LE>(lds, E, p0, add_raw_reduce(s02, s13));
+    Fr y1, y3;
+    root_mul_pair(sub_raw6(s02, s13), j, rsub(d02, d13), j, ltw, y1, y3);
+    lds_put<LE>(lds, E, p1, y1);
+    lds_put<LE>(lds, E, p3, y3);
+  } else {  // last pair (span 1): no multiply in stage t+1
+    const Fr s02 = add(x0, x2), s13 = add(x1, x3);
+    lds_put<LE>(lds, E, p0, add(s02, s13));
+    lds_put<LE>(lds, E, p1, sub(s02, s13));
+    lds_put<LE>(lds, E, p3, stage_sub(d02, d13));
+  }
+  lds_put<LE>(lds, E, p2, add(d02, d13));
+#else
   const Fr d02 = bfly_d(x0, x2, ltw, i << t);
   const Fr d13 = bfly_d(x1, x3, ltw, (i + Hh) << t);
   const uint32_t j = i << (t + 1);
@@ -246,6 +288,7 @@ __device__ __forceinline__ void r4_unit(uint32_t* __restrict__ lds, const uint32
   }
   lds_put<LE>(lds, E, p2, add(d02, d13));
   lds_put<LE>(lds, E, p3, bfly_d(d02, d13, ltw, j));
+#endif
 #endif
 }
 
