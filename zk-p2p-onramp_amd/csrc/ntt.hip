@@ -364,35 +364,75 @@ __global__ __launch_bounds__(TPB) NTT_WPE_ATTR void k_ntt(uint32_t* __restrict__
   const int E = LE ? (1 << LE) : (1 << (T.b + T.lc + T.lbt));  // LE: the tile size known at compile time
   const uint32_t tile = blockIdx.x;
   stage_roots(ltw, rootsA, locA, T.b);
-  for (int e = threadIdx.x; e < E; e += TPB) {
-    size_t g;
-    uint32_t pos;
-    tile_coords(T, tile, e, g, pos);
-    Fr x = load_fe<FrCfg>(data + g * 8);
-    if (MODE == 1 && tw) x = mul(x, load_fe<FrCfg>(tw + (size_t)pos * 8));
+  constexpr int VPT = (1 << LOG_TILE) / TPB;  // elements per thread of a full tile
+  if (LE && MODE == 1 && tw) {
+    // full tiles: the twiddle products of two elements at a time in lockstep (mul_pair)
 #pragma unroll
-    for (int l = 0; l < NL; ++l) lds[l * E + swz(e)] = x.v[l];
+    for (int it = 0; it < VPT; it += 2) {
+      const int e0 = (int)threadIdx.x + it * TPB, e1 = e0 + TPB;
+      size_t g0, g1;
+      uint32_t pos0, pos1;
+      tile_coords(T, tile, e0, g0, pos0);
+      tile_coords(T, tile, e1, g1, pos1);
+      Fr x0, x1;
+      mul_pair(load_fe<FrCfg>(data + g0 * 8), load_fe<FrCfg>(tw + (size_t)pos0 * 8), load_fe<FrCfg>(data + g1 * 8),
+               load_fe<FrCfg>(tw + (size_t)pos1 * 8), x0, x1);
+#pragma unroll
+      for (int l = 0; l < NL; ++l) {
+        lds[l * E + swz(e0)] = x0.v[l];
+        lds[l * E + swz(e1)] = x1.v[l];
+      }
+    }
+  } else {
+    for (int e = threadIdx.x; e < E; e += TPB) {
+      size_t g;
+      uint32_t pos;
+      tile_coords(T, tile, e, g, pos);
+      Fr x = load_fe<FrCfg>(data + g * 8);
+      if (MODE == 1 && tw) x = mul(x, load_fe<FrCfg>(tw + (size_t)pos * 8));
+#pragma unroll
+      for (int l = 0; l < NL; ++l) lds[l * E + swz(e)] = x.v[l];
+    }
   }
   __syncthreads();
   dft_stages<LE>(lds, ltw, E, T.b, T.lc);
   if (MODE == 2) {
     // output row k1 (natural position in the block) sits at LDS row brev(k1): key it with
     // g^f(pos)/n and put it back at row k1 as the forward DFT's input
-    // (a fixed trip count keeps v[] in registers: a runtime-indexed array went to scratch)
-    constexpr int VPT = (1 << LOG_TILE) / TPB;
+    // (a fixed trip count keeps v[] in registers: a runtime-indexed array went to scratch; full
+    // tiles key two elements at a time in lockstep)
     Fr v[VPT];
+    if (LE) {
 #pragma unroll
-    for (int it = 0; it < VPT; ++it) {
-      const int e = (int)threadIdx.x + it * TPB;
-      if (e < E) {
-        const int src = swz(brev_src(T, e));
-        Fr x;
+      for (int it = 0; it < VPT; it += 2) {
+        const int e0 = (int)threadIdx.x + it * TPB, e1 = e0 + TPB;
+        const int src0 = swz(brev_src(T, e0)), src1 = swz(brev_src(T, e1));
+        Fr x0, x1;
 #pragma unroll
-        for (int l = 0; l < NL; ++l) x.v[l] = lds[l * E + src];
-        size_t g;
-        uint32_t pos;
-        tile_coords(T, tile, e, g, pos);
-        v[it] = mul(x, load_fe<FrCfg>(coset + g * 8));
+        for (int l = 0; l < NL; ++l) {
+          x0.v[l] = lds[l * E + src0];
+          x1.v[l] = lds[l * E + src1];
+        }
+        size_t g0, g1;
+        uint32_t pos0, pos1;
+        tile_coords(T, tile, e0, g0, pos0);
+        tile_coords(T, tile, e1, g1, pos1);
+        mul_pair(x0, load_fe<FrCfg>(coset + g0 * 8), x1, load_fe<FrCfg>(coset + g1 * 8), v[it], v[it + 1]);
+      }
+    } else {
+#pragma unroll
+      for (int it = 0; it < VPT; ++it) {
+        const int e = (int)threadIdx.x + it * TPB;
+        if (e < E) {
+          const int src = swz(brev_src(T, e));
+          Fr x;
+#pragma unroll
+          for (int l = 0; l < NL; ++l) x.v[l] = lds[l * E + src];
+          size_t g;
+          uint32_t pos;
+          tile_coords(T, tile, e, g, pos);
+          v[it] = mul(x, load_fe<FrCfg>(coset + g * 8));
+        }
       }
     }
     __syncthreads();
@@ -408,16 +448,38 @@ __global__ __launch_bounds__(TPB) NTT_WPE_ATTR void k_ntt(uint32_t* __restrict__
     __syncthreads();
     dft_stages<LE>(lds, ltw, E, T.b, T.lc);
   }
-  for (int e = threadIdx.x; e < E; e += TPB) {
-    const int src = swz(brev_src(T, e));
-    Fr x;
+  if (LE && MODE == 0 && tw) {
 #pragma unroll
-    for (int l = 0; l < NL; ++l) x.v[l] = lds[l * E + src];
-    size_t g;
-    uint32_t pos;
-    tile_coords(T, tile, e, g, pos);
-    if (MODE == 0 && tw) x = mul(x, load_fe<FrCfg>(tw + (size_t)pos * 8));
-    store_fe(data + g * 8, x);
+    for (int it = 0; it < VPT; it += 2) {
+      const int e0 = (int)threadIdx.x + it * TPB, e1 = e0 + TPB;
+      const int src0 = swz(brev_src(T, e0)), src1 = swz(brev_src(T, e1));
+      Fr x0, x1;
+#pragma unroll
+      for (int l = 0; l < NL; ++l) {
+        x0.v[l] = lds[l * E + src0];
+        x1.v[l] = lds[l * E + src1];
+      }
+      size_t g0, g1;
+      uint32_t pos0, pos1;
+      tile_coords(T, tile, e0, g0, pos0);
+      tile_coords(T, tile, e1, g1, pos1);
+      Fr y0, y1;
+      mul_pair(x0, load_fe<FrCfg>(tw + (size_t)pos0 * 8), x1, load_fe<FrCfg>(tw + (size_t)pos1 * 8), y0, y1);
+      store_fe(data + g0 * 8, y0);
+      store_fe(data + g1 * 8, y1);
+    }
+  } else {
+    for (int e = threadIdx.x; e < E; e += TPB) {
+      const int src = swz(brev_src(T, e));
+      Fr x;
+#pragma unroll
+      for (int l = 0; l < NL; ++l) x.v[l] = lds[l * E + src];
+      size_t g;
+      uint32_t pos;
+      tile_coords(T, tile, e, g, pos);
+      if (MODE == 0 && tw) x = mul(x, load_fe<FrCfg>(tw + (size_t)pos * 8));
+      store_fe(data + g * 8, x);
+    }
   }
 }
 
