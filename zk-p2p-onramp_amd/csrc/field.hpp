@@ -389,6 +389,59 @@ ZDEV void mul_pair(const Fe<C>& a, const Fe<C>& b, const Fe<C>& c, const Fe<C>& 
   s.v[NL - 1] = (uint32_t)y;
 }
 
+// Two lazily reduced sums of N products, r = sum_k a[k] b[k], s = sum_k c[k] d[k] (mul2 / mul4 each),
+// in lockstep with chained columns when CH: the Fq2 products of the G2 arithmetic (c0 and c1 of a
+// product, ZKP_CHAIN_G2).  Operand conditions as mul2 / mul4.
+template <class C, bool CH, int N>
+ZDEV void sop_pair(const Fe<C>* const (&a)[N], const Fe<C>* const (&b)[N], const Fe<C>* const (&c)[N],
+                   const Fe<C>* const (&d)[N], Fe<C>& r, Fe<C>& s) {
+  uint32_t m[NL], n[NL];
+  uint64_t x = 0, y = 0;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) {
+#pragma unroll
+    for (int j = 0; j < i; ++j) {
+#pragma unroll
+      for (int k = 0; k < N; ++k) {
+        mac<CH>(x, a[k]->v[j], b[k]->v[i - j]);
+        mac<CH>(y, c[k]->v[j], d[k]->v[i - j]);
+      }
+      mac_k<CH>(x, m[j], C::MOD[i - j]);
+      mac_k<CH>(y, n[j], C::MOD[i - j]);
+    }
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+      mac<CH>(x, a[k]->v[i], b[k]->v[0]);
+      mac<CH>(y, c[k]->v[i], d[k]->v[0]);
+    }
+    m[i] = ((uint32_t)x * C::INV) & LMASK;
+    n[i] = ((uint32_t)y * C::INV) & LMASK;
+    mac_k<CH>(x, m[i], C::MOD[0]);
+    mac_k<CH>(y, n[i], C::MOD[0]);
+    x >>= LB;
+    y >>= LB;
+  }
+#pragma unroll
+  for (int i = NL; i < 2 * NL - 1; ++i) {
+#pragma unroll
+    for (int j = i - NL + 1; j < NL; ++j) {
+#pragma unroll
+      for (int k = 0; k < N; ++k) {
+        mac<CH>(x, a[k]->v[j], b[k]->v[i - j]);
+        mac<CH>(y, c[k]->v[j], d[k]->v[i - j]);
+      }
+      mac_k<CH>(x, m[j], C::MOD[i - j]);
+      mac_k<CH>(y, n[j], C::MOD[i - j]);
+    }
+    r.v[i - NL] = (uint32_t)x & LMASK;
+    s.v[i - NL] = (uint32_t)y & LMASK;
+    x >>= LB;
+    y >>= LB;
+  }
+  r.v[NL - 1] = (uint32_t)x;
+  s.v[NL - 1] = (uint32_t)y;
+}
+
 // three independent products in lockstep (two other mads between dependent ones of a chain)
 template <class C>
 ZDEV void mul_triple(const Fe<C>& a, const Fe<C>& b, const Fe<C>& c, const Fe<C>& d, const Fe<C>& e, const Fe<C>& f,
@@ -921,18 +974,39 @@ ZDEV Fq neg4(const Fq& a) {
 // (a0 + a1 u)(b0 + b1 u) = (a0 b0 - a1 b1) + (a0 b1 + a1 b0) u as two lazily reduced sums
 // of products (2 x 162 + 2 x 81 mads, like Karatsuba's 3 x 162, but no Karatsuba adds and
 // subtractions: ~650 instead of ~1100 instructions).  Components normalised, < 4m.
+// ZKP_CHAIN_G2 (default on): the two components' sums of products run in lockstep with chained
+// columns (sop_pair); 0: two independent mul2 / mul4 as the compiler schedules them
+#ifndef ZKP_CHAIN_G2
+#define ZKP_CHAIN_G2 1
+#endif
 ZDEV Fq2 mul(const Fq2& a, const Fq2& b) {
   Fq2 r;
+#if ZKP_CHAIN_G2
+  const Fq nb1 = neg4(b.c1);
+  const Fq* x0[2] = {&a.c0, &a.c1};
+  const Fq* y0[2] = {&b.c0, &nb1};
+  const Fq* y1[2] = {&b.c1, &b.c0};
+  sop_pair<FqCfg, true, 2>(x0, y0, x0, y1, r.c0, r.c1);
+#else
   r.c0 = mul2(a.c0, b.c0, a.c1, neg4(b.c1));
   r.c1 = mul2(a.c0, b.c1, a.c1, b.c0);
+#endif
   return r;
 }
 
 // a*b + c*d in Fq2 with two lazily reduced four-product sums
 ZDEV Fq2 mul2(const Fq2& a, const Fq2& b, const Fq2& c, const Fq2& d) {
   Fq2 r;
+#if ZKP_CHAIN_G2
+  const Fq nb1 = neg4(b.c1), nd1 = neg4(d.c1);
+  const Fq* x[4] = {&a.c0, &a.c1, &c.c0, &c.c1};
+  const Fq* y0[4] = {&b.c0, &nb1, &d.c0, &nd1};
+  const Fq* y1[4] = {&b.c1, &b.c0, &d.c1, &d.c0};
+  sop_pair<FqCfg, true, 4>(x, y0, x, y1, r.c0, r.c1);
+#else
   r.c0 = mul4(a.c0, b.c0, a.c1, neg4(b.c1), c.c0, d.c0, c.c1, neg4(d.c1));
   r.c1 = mul4(a.c0, b.c1, a.c1, b.c0, c.c0, d.c1, c.c1, d.c0);
+#endif
   return r;
 }
 
@@ -955,7 +1029,18 @@ ZDEV Fq2 lsub4_lazy(const Fq2& a, const Fq2& b) { return Fq2{lsub4(a.c0, b.c0), 
 // a^2 for components < 6m: (a0 + a1)(a0 - a1 + 6m) [raw sum x normalised, < 144 m^2] and
 // (2 a0) a1 [raw x normalised, < 72 m^2] -- no additions reduced, no doubling of the product
 ZDEV Fq2 sqr_lazy(const Fq2& a) {
+#if ZKP_CHAIN_G2
+  const Fq s = add_raw(a.c0, a.c1), d = lsub6(a.c0, a.c1), t = shl1_raw(a.c0);
+  const Fq* x0[1] = {&s};
+  const Fq* y0[1] = {&d};
+  const Fq* x1[1] = {&t};
+  const Fq* y1[1] = {&a.c1};
+  Fq2 r;
+  sop_pair<FqCfg, true, 1>(x0, y0, x1, y1, r.c0, r.c1);
+  return r;
+#else
   return Fq2{mul(add_raw(a.c0, a.c1), lsub6(a.c0, a.c1)), mul(shl1_raw(a.c0), a.c1)};
+#endif
 }
 // R^2 - PPP - 2Q per component (each < 2m) -> < 4m: one conditional subtraction instead of two.
 // (Not qreduce: its single 27-deep dependent chain per component measured 6 % slower in the
