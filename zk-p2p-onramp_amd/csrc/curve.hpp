@@ -289,14 +289,13 @@ ZDEV void xyzz_add(Xyzz<F>& acc, const Xyzz<F>& q) {
     acc = q;
     return;
   }
-  F U1 = mul(acc.x, q.zz);
-  F U2 = mul(q.x, acc.zz);
-  F S1 = mul(acc.y, q.zzz);
-  F S2 = mul(q.y, acc.zzz);
+  F U1, U2, S1, S2;
+  mul_2(acc.x, q.zz, q.x, acc.zz, U1, U2);
+  mul_2(acc.y, q.zzz, q.y, acc.zzz, S1, S2);
   F P = acc_sub(U2, U1);
   F R = acc_sub(S2, S1);
-  F PP = acc_sqr(P);
-  F RR = acc_sqr(R);
+  F PP, RR;
+  acc_sqr_2(P, R, PP, RR);
   if (is_zero(PP)) {
     if (is_zero(RR))
       acc = xyzz_dbl(acc);
@@ -304,12 +303,13 @@ ZDEV void xyzz_add(Xyzz<F>& acc, const Xyzz<F>& q) {
       acc = xyzz_inf<F>();
     return;
   }
-  F PPP = mul(P, PP);
-  F Q = mul(U1, PP);
+  F PPP, Q;
+  mul_2(P, PP, U1, PP, PPP, Q);
   F X3 = acc_x3(RR, PPP, Q);
   F Y3 = acc_y3(R, acc_xsub(Q, X3), S1, acc_negd(PPP));  // R (Q - X3) - S1 PPP
-  acc.zz = mul(mul(acc.zz, q.zz), PP);
-  acc.zzz = mul(mul(acc.zzz, q.zzz), PPP);
+  F ZZ, ZZZ;
+  mul_2(acc.zz, q.zz, acc.zzz, q.zzz, ZZ, ZZZ);
+  mul_2(ZZ, PP, ZZZ, PPP, acc.zz, acc.zzz);
   acc.x = X3;
   acc.y = Y3;
 }

@@ -1,6 +1,7 @@
 // Per-thread bodies of the MSM kernels (__host__ __device__ so that
 // tools/hosttest/msm_emu.cpp can replay the exact pipeline on the CPU).
 #pragma once
+#include <type_traits>
 #include "curve.hpp"
 
 namespace zkp {
@@ -136,6 +137,16 @@ struct AccField<Fq> {
   using type = Fe<FqAccCfg>;
 };
 
+// the field of the merge and reduction kernels (full XYZZ additions, latency-bound chains):
+// ZKP_MERGE_CHAIN=1 gives them the accumulation's chained columns and lockstep product pairs
+#ifndef ZKP_MERGE_CHAIN
+#define ZKP_MERGE_CHAIN 1
+#endif
+template <class F>
+struct MergeField {
+  using type = typename std::conditional<ZKP_MERGE_CHAIN != 0, typename AccField<F>::type, F>::type;
+};
+
 // thread i runs task perm[i] (tasks ordered by length, longest first: the lanes of a wave run
 // equally long chains) or task i (perm == nullptr)
 template <class FS>
@@ -209,10 +220,11 @@ ZDEV void heavy_counts(uint32_t b, const uint32_t* __restrict__ off, uint32_t nb
 }
 
 // merge task t of level lvl: sums <= S2 consecutive partials of one heavy bucket
-template <class F>
+template <class FS>
 ZDEV void merge_heavy(uint32_t t, const uint32_t* __restrict__ src, const uint32_t* __restrict__ off,
                       const uint32_t* __restrict__ hoff, uint32_t nb, uint32_t S2, int lvl,
                       uint32_t* __restrict__ dst) {
+  using F = typename MergeField<FS>::type;
   if (t >= hoff[nb]) return;
   const uint32_t b = seg_search(hoff, nb, t);
   const uint32_t j = t - hoff[b];
@@ -226,10 +238,11 @@ ZDEV void merge_heavy(uint32_t t, const uint32_t* __restrict__ src, const uint32
 }
 
 // one thread per bucket: fold its (<= 2*S2) remaining partials into buckets[b] (infinity if none)
-template <class F>
+template <class FS>
 ZDEV void merge_final(uint32_t b, const uint32_t* __restrict__ part0, const uint32_t* __restrict__ part1,
                       const uint32_t* __restrict__ off, uint32_t nb, uint32_t S2, int levels,
                       uint32_t* __restrict__ buckets) {
+  using F = typename MergeField<FS>::type;
   if (b >= nb) return;
   int applied;
   const uint32_t c = merged_count(off[b + 1] - off[b], S2, levels, applied);
@@ -246,9 +259,10 @@ ZDEV void merge_final(uint32_t b, const uint32_t* __restrict__ part0, const uint
 // short add chains instead of one long running sum; the host applies the 2^b / M weights.
 
 // segment p of group g (one thread): S_p, T_p by running sums over M buckets
-template <class F>
+template <class FS>
 ZDEV void reduce_segments(uint32_t id, const uint32_t* __restrict__ buckets, uint32_t G, uint32_t half, uint32_t M,
                           uint32_t* __restrict__ s_out, uint32_t* __restrict__ t_out) {
+  using F = typename MergeField<FS>::type;
   const uint32_t P = half / M;
   if (id >= G * P) return;
   const uint32_t g = id / P, p = id - g * P;
@@ -270,9 +284,10 @@ ZDEV uint32_t subset_n1(uint32_t lgP, uint32_t fan) {
 // first level of the K = lgP + 1 subset sums of group g: sum b < lgP over the P/2 values
 // S_p with bit b of p set (fan consecutive per thread), sum lgP over all P values T_p
 // (2*fan per thread).  out[(g*K + b)*n1 + j]
-template <class F>
+template <class FS>
 ZDEV void subset_first(uint32_t id, const uint32_t* __restrict__ s_in, const uint32_t* __restrict__ t_in,
                        uint32_t G, uint32_t lgP, uint32_t fan, uint32_t* __restrict__ out) {
+  using F = typename MergeField<FS>::type;
   const uint32_t P = 1u << lgP, K = lgP + 1, n1 = subset_n1(lgP, fan);
   if (id >= G * K * n1) return;
   const uint32_t seg = id / n1, j = id - seg * n1, g = seg / K, b = seg - g * K;
@@ -291,9 +306,10 @@ ZDEV void subset_first(uint32_t id, const uint32_t* __restrict__ s_in, const uin
 }
 
 // next level: nseg segments of n_in values -> n_out = ceil(n_in / fan) sums of fan consecutive
-template <class F>
+template <class FS>
 ZDEV void subset_level(uint32_t id, const uint32_t* __restrict__ in, uint32_t nseg, uint32_t n_in, uint32_t fan,
                        uint32_t* __restrict__ out) {
+  using F = typename MergeField<FS>::type;
   const uint32_t n_out = (n_in + fan - 1) / fan;
   if (id >= nseg * n_out) return;
   const uint32_t seg = id / n_out, j = id - seg * n_out;
