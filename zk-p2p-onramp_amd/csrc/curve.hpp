@@ -154,6 +154,15 @@ ZDEV Xyzz<F> xyzz_inf() {
 template <class F>
 ZDEV bool xyzz_is_inf(const Xyzz<F>& p) { return is_zero_raw(p.zz); }
 
+// one-limb screens of the exact zero tests: lo_zero(a) is necessary for a == 0 (raw), maybe_zero(a)
+// for a normalised a < 2m to be 0 or m (is_zero)
+template <class C>
+ZDEV bool lo_zero(const Fe<C>& a) { return a.v[0] == 0; }
+ZDEV bool lo_zero(const Fq2& a) { return a.c0.v[0] == 0 && a.c1.v[0] == 0; }
+template <class C>
+ZDEV bool maybe_zero(const Fe<C>& a) { return a.v[0] == 0 || a.v[0] == C::MOD[0]; }
+ZDEV bool maybe_zero(const Fq2& a) { return maybe_zero(a.c0) && maybe_zero(a.c1); }
+
 template <class F>
 ZDEV bool aff_is_inf(const Aff<F>& p) { return is_zero_raw(p.x) && is_zero_raw(p.y); }
 
@@ -208,13 +217,19 @@ ZDEV Xyzz<F> xyzz_dbl(const Xyzz<F>& p_in) {
 // a multiplication; zero tests run on PP = P^2 and RR = R^2, which are < 2m.
 template <class F>
 ZDEV void xyzz_add_aff(Xyzz<F>& acc, const Aff<F>& q, bool neg = false) {
-  if (aff_is_inf(q)) return;
-  if (xyzz_is_inf(acc)) {
-    acc.x = q.x;
-    acc.y = neg ? sub(f_zero<F>(), q.y) : q.y;
-    acc.zz = f_one<F>();
-    acc.zzz = f_one<F>();
-    return;
+  // the exceptional cases (a base at infinity, an empty accumulator, P = +-Q below) are screened
+  // by their low limb first: the exact tests run only where it allows them, never on the common path
+  if (lo_zero(q.x) && lo_zero(q.y)) {
+    if (aff_is_inf(q)) return;
+  }
+  if (lo_zero(acc.zz)) {
+    if (xyzz_is_inf(acc)) {
+      acc.x = q.x;
+      acc.y = neg ? sub(f_zero<F>(), q.y) : q.y;
+      acc.zz = f_one<F>();
+      acc.zzz = f_one<F>();
+      return;
+    }
   }
   const F qy = neg ? rsub(f_zero<F>(), q.y) : q.y;  // mul operand only
   F U2, S2;
@@ -223,15 +238,17 @@ ZDEV void xyzz_add_aff(Xyzz<F>& acc, const Aff<F>& q, bool neg = false) {
   F R = acc_sub(S2, acc.y);
   F PP, RR;
   acc_sqr_2(P, R, PP, RR);
-  if (is_zero(PP)) {
-    if (is_zero(RR)) {
-      Aff<F> qs = q;
-      if (neg) qs.y = sub(f_zero<F>(), q.y);
-      acc = xyzz_dbl_aff(qs);
-    } else {
-      acc = xyzz_inf<F>();
+  if (maybe_zero(PP)) {
+    if (is_zero(PP)) {
+      if (is_zero(RR)) {
+        Aff<F> qs = q;
+        if (neg) qs.y = sub(f_zero<F>(), q.y);
+        acc = xyzz_dbl_aff(qs);
+      } else {
+        acc = xyzz_inf<F>();
+      }
+      return;
     }
-    return;
   }
   F PPP, Q, ZZ3, ZZZ3, Y3;
   if (ZKP_MUL_PAIRS >= 2) {
