@@ -448,11 +448,12 @@ class DevicePipeline {
   int device() const { return dev_; }
 
   // quotient (rows A4..A8) from a device-resident witness; result scalars in pscal_
-  void enqueue_quotient(const uint32_t* d_wit) {
+  void enqueue_quotient(const uint32_t* d_wit, const std::function<void()>& before_ntt = {}) {
     const ZkeyHeader& h = hdr_;
     launch_build_abc(rowptr_[0], col_[0], val_[0], rowptr_[1], col_[1], val_[1], d_wit, h.domain_size, abc_[0],
                      abc_[1], abc_[2], s0_);
     HIPX(hipEventRecord(ev_[2], s0_));
+    if (before_ntt) before_ntt();
     for (auto* b : abc_) ntt_->coset_extend(b);
     launch_join_abc(abc_[0], abc_[1], abc_[2], h.domain_size, pscal_, s0_);
     HIPX(hipEventRecord(ev_[3], s0_));
@@ -681,6 +682,13 @@ class DevicePipeline {
           HIPX(hipEventRecord(ev_[2], s0_));
           launch_join_abc(ext_abc_[0], ext_abc_[1], ext_abc_[2], (uint32_t)(hhi_ - hlo_), pscal_ + hlo_ * 8, s0_);
           HIPX(hipEventRecord(ev_[3], s0_));
+        } else if (!serial_ && ntt_after_wplan_) {
+          // experiment: the NTTs wait for the witness plan, so its sort is not starved by them
+          // and the witness accumulations start beside the NTTs
+          enqueue_quotient(d_wit, [&] {
+            planned_f.get();
+            HIPX(hipStreamWaitEvent(s0_, plan_w_->ready(), 0));
+          });
         } else {
           enqueue_quotient(d_wit);
         }
@@ -763,6 +771,7 @@ class DevicePipeline {
   bool serial_ = std::getenv("ZKP_SERIAL") && std::getenv("ZKP_SERIAL")[0] == '1';  // profiling: no stream overlap
   int gate_mode_ = env_int("ZKP_SCHED", 0);
   int g2_finish_gate_ = env_int("ZKP_G2_FINISH_GATE", 0);
+  bool ntt_after_wplan_ = env_int("ZKP_NTT_AFTER_WPLAN", 0) == 1;
   bool sched_gate_ = gate_mode_ != 0;
   ZkeyHeader hdr_;
   hipStream_t s0_ = nullptr, s1_ = nullptr, s2_ = nullptr, s3_ = nullptr;
