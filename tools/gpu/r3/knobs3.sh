@@ -9,7 +9,7 @@ run() {
   env "$@" timeout -k 10 300 $B > gpurun_out/b_k.log 2>&1
   echo "$* $(tail -1 gpurun_out/b_k.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); s=d["stage_ms_last_proof"]; print(d["ms_per_step"], s["msm_g1_abc"], s["msm_g2"], s["msm_g1_h"], d["all_proofs_ok"])')" >> gpurun_out/knobs3.txt
 }
-for i in 1 2 3 4; do
+for i in 1 2 3; do
   run ZKP_NONE=0
   run ZKP_TASK_H=48
   run ZKP_TASK_H=48 ZKP_TASK_W=48
