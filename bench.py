@@ -323,8 +323,87 @@ def batch_pcie_inclusive(args, circ, prover, wit, refs, rank, world, ndev, dist,
             "check": "every batch proof == a separately computed proof of the same witness at the same r, s",
             "pipelines_per_device": int(os.environ.get("ZKP_INFLIGHT", "1")),
             "workers_per_pipeline": 2,
-            "note": "zkp_prove_batch from pageable host memory over %d device(s): the 205 MB witness H2D of "
-                    "proof i+1 runs on an upload-slot stream while proof i computes" % ndev}
+            "note": "zkp_prove_batch from pageable host memory over %d device(s): the 205 MB witness upload of "
+                    "proof i+1 (pinned slot, copy stream) runs while proof i computes" % ndev}
+
+
+def accumulate_rooflines(launches, peak, peak_src, traffic):
+    """Per-launch roofline of the bucket-accumulate kernels (HIP events around every timed launch,
+    zkp_prover_launch_stats).  The headline `roofline` is the H MSM's launch, which runs with the
+    GPU mostly to itself at the end of the proof; the witness launches (A, B1, C: beside the quotient
+    and the other streams) and the G2 launch (B2) are reported per launch kind.  Algorithmic work per
+    mixed addition: G1 11 Fp-mul x 136 MAC, G2 3x that (Fq2)."""
+    kinds = {}
+    for r in launches:
+        kinds.setdefault(r["msm"], []).append(r)
+
+    def line(rs, mult, kernel):
+        adds = sum(r["adds"] for r in rs) / len(rs)
+        ms = sum(r["ms"] for r in rs) / len(rs)
+        mac = adds * FPMUL_PER_MADD * MAC_PER_FPMUL * mult
+        ach = mac / (ms * 1e-3) / 1e12 if ms > 0 else None
+        return {"kernel": kernel, "launches": len(rs), "mixed_adds_per_launch": int(adds),
+                "avg_launch_ms": round(ms, 4), "ms_min": round(min(r["ms"] for r in rs), 4),
+                "ms_max": round(max(r["ms"] for r in rs), 4),
+                "achieved": round(ach, 3) if ach else None, "frac": round(ach / peak, 4) if (ach and peak) else None}
+    lines = {}
+    for k in ("A", "B1", "C", "H"):
+        if k in kinds:
+            lines[k] = line(kinds[k], 1, "k_accumulate<Fq>")
+    if "B2" in kinds:
+        lines["B2"] = line(kinds["B2"], 3, "k_accumulate<Fq2>")
+    h = lines.get("H") or {}
+    roofline = {
+        "kernel": "k_accumulate<Fq>, the H MSM launch (G1 bucket accumulation, XYZZ mixed adds)",
+        "bound": "valu-int",
+        "achieved": h.get("achieved"),
+        "peak": peak,
+        "unit": "TMAC/s (32x32->64 v_mad_u64_u32)",
+        "frac": h.get("frac"),
+        "traffic": traffic.get("hbm_bytes_per_launch") if traffic else None,
+        "traffic_source": traffic.get("source") if traffic else None,
+        "algorithmic_work_per_launch": {"mixed_adds": h.get("mixed_adds_per_launch"), "fp_mul_per_add": FPMUL_PER_MADD,
+                                        "mac_per_fp_mul": MAC_PER_FPMUL},
+        "valu_issue_frac_pmc": traffic.get("valu_issue_frac") if traffic else None,
+        "avg_launch_ms": h.get("avg_launch_ms"),
+        "launches_timed": h.get("launches"),
+        "peak_source": peak_src,
+        "note": "integer-multiply (VALU) bound, no MFMA/HBM bound applies (SURVEY.md §8d D3); frac counts the "
+                "algorithmic 136 MAC per Fp mul; per-launch-kind lines in roofline_launches (A, B1, C, B2 share "
+                "the GPU with the quotient and the other streams)",
+    }
+    if traffic and h.get("avg_launch_ms"):
+        # traffic is the PMC average over all G1 launches; reported against the H launch time
+        roofline["hbm_GBps"] = round(traffic["hbm_bytes_per_launch"] / (h["avg_launch_ms"] * 1e-3) / 1e9, 1)
+    g2 = lines.get("B2")
+    roofline_g2 = None
+    if g2:
+        roofline_g2 = dict(g2, bound="valu-int", peak=peak, unit="TMAC/s (32x32->64 v_mad_u64_u32)",
+                           work="3 x the G1 unit per Fq2 mixed addition (SURVEY.md §8d D4)")
+    return roofline, {"per_kind": lines, "roofline_g2": roofline_g2}
+
+
+def bool0_line(args, device, r_fix, s_fix, steps=4):
+    """The bound of the witness assumption: the Venmo-shaped circuit with every defined signal uniform
+    (bool_pct 0: the witness MSMs then carry ~W digits per signal instead of ~1.6), its own key, staged
+    witnesses, on a prover of its own (the caller releases the headline prover first)."""
+    c0 = synth.Circuit.venmo(CIRCUIT_SEED, bool_pct=0)
+    ws = gen_witnesses(c0, [900001 + i for i in range(2)])
+    zk = c0.zkey(SETUP_SEED, device=device)
+    p = zkp_amd.Prover(zk, devices=[device])
+    for i, w in enumerate(ws):
+        p.stage(w, slot=i)
+    p.prove_staged_raw(0, r_fix, s_fix)
+    ref = [p.prove_raw(w, r_fix, s_fix) for w in ws]
+    t0 = time.perf_counter()
+    res = [p.prove_staged_raw(i % 2, r_fix, s_fix) for i in range(steps)]
+    el = time.perf_counter() - t0
+    ok = all(r == ref[i % 2] for i, r in enumerate(res))
+    p.close()
+    return {"witness_bool_pct": 0, "proofs_per_s": round(steps / el, 3), "ms_per_proof": round(el / steps * 1e3, 3),
+            "steps": steps, "all_proofs_ok": ok,
+            "note": "Venmo shape, every defined signal uniform (its own key; the worst case of the witness "
+                    "MSMs); the headline assumes 70 % bit-valued signals"}
 
 
 def cpu_baseline(args, zk, wit0, gpu_proof, r_fix, s_fix, msm_case):
@@ -379,6 +458,8 @@ def main():
     ap.add_argument("--bool-pct", type=int, default=70,
                     help="witness mix: percent of bit-valued (AND/XOR) signals; 70 = the default assumption, "
                          "0 = all-uniform witness (sensitivity of the witness MSMs to the real witness)")
+    ap.add_argument("--no-bool0-line", dest="bool0_line", action="store_false",
+                    help="skip the all-uniform-witness sub-line (the bound of the witness assumption)")
     ap.add_argument("--scale", type=float, default=1.0, help="fraction of the Venmo shape (smoke/debug only)")
     ap.add_argument("--quotient", choices=["dist", "full"], default="dist",
                     help="split mode: distribute the three coset extensions over the ranks, or recompute per rank")
@@ -514,10 +595,20 @@ def main():
     msm_cfg = prover.msm_config()
     stage_ms = prover.timings()
 
-    # H2D-inclusive latency of one proof from a host witness (reported beside, never `value`)
-    t0 = time.perf_counter()
-    prover.prove_raw(wit[0], R_FIX, S_FIX)
-    pcie_latency_ms = (time.perf_counter() - t0) * 1e3
+    launches = prover.launch_stats()
+    # 1-proof latency from a HOST witness (the reference call: zkp.ts:94, 5_gen_proof.sh:8): upload
+    # through the pinned slot + proof + assembly, one proof at a time (median of 5, each checked)
+    lat, up_ms = [], []
+    for i in range(5):
+        t0 = time.perf_counter()
+        pr = prover.prove_raw(wit[i % nw], R_FIX, S_FIX)
+        lat.append((time.perf_counter() - t0) * 1e3)
+        up_ms.append(prover.timings()["wtns_h2d"])
+        if pr != refs[i % nw]:
+            mismatch.append(("host-witness latency proof", i))
+    lat.sort()
+    up_ms.sort()
+    pcie_latency_ms, upload_ms = lat[len(lat) // 2], up_ms[len(up_ms) // 2]
 
     batch = None
     if args.batch > 0:
@@ -529,35 +620,10 @@ def main():
     n_total = args.steps * world * ndev
     value = n_total / elapsed
     ms_per_step = elapsed / args.steps * 1e3
-    g1 = kstats["g1"]
-    acc_ms = g1["accumulate_ms"] / max(1, g1["launches"])
-    adds = g1["mixed_adds"] / max(1, g1["launches"])
     peak, peak_src = load_peak()
-    achieved = adds * FPMUL_PER_MADD * MAC_PER_FPMUL / (acc_ms * 1e-3) / 1e12 if acc_ms > 0 else None
     traffic = load_traffic()
-    roofline = {
-        "kernel": "k_accumulate<Fq> (G1 bucket accumulation, XYZZ mixed adds)",
-        "bound": "valu-int",
-        "achieved": round(achieved, 3) if achieved else None,
-        "peak": peak,
-        "unit": "TMAC/s (32x32->64 v_mad_u64_u32)",
-        "frac": round(achieved / peak, 4) if (achieved and peak) else None,
-        "traffic": traffic.get("hbm_bytes_per_launch") if traffic else None,
-        "traffic_source": traffic.get("source") if traffic else None,
-        "algorithmic_work_per_launch": {"mixed_adds": int(adds), "fp_mul_per_add": FPMUL_PER_MADD,
-                                        "mac_per_fp_mul": MAC_PER_FPMUL},
-        "valu_issue_frac_pmc": traffic.get("valu_issue_frac") if traffic else None,
-        # point streaming: PMC HBM bytes per launch over the live average launch time, against 8 TB/s
-        "hbm_GBps": round(traffic["hbm_bytes_per_launch"] / (acc_ms * 1e-3) / 1e9, 1) if (traffic and acc_ms > 0) else None,
-        "hbm_frac_of_8TBps": round(traffic["hbm_bytes_per_launch"] / (acc_ms * 1e-3) / 8e12, 4) if (traffic and acc_ms > 0) else None,
-        "note": "integer-multiply (VALU) bound, no MFMA/HBM bound applies (SURVEY.md §8d D3); frac counts the "
-                "algorithmic 136 MAC per Fp mul, the kernel issues ~2.7x that in VALU instructions (29-bit-limb "
-                "FIPS product scanning: 162 mads + carries per mul, plus adds/subs) at valu_issue_frac_pmc of the "
-                "measured issue peak",
-        "avg_launch_ms": round(acc_ms, 4),
-        "launches_timed": g1["launches"],
-        "peak_source": peak_src,
-    }
+    roofline, acc_lines = accumulate_rooflines(launches, peak, peak_src, traffic)
+    wit_bytes = circ.n_vars * 32
 
     out = {
         "metric": "Groth16 proofs/sec (node) + 1-proof latency, Venmo circuit; G1 MSM Mpts/s",
@@ -567,8 +633,15 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 3),
-        "latency_ms": round(ms_per_step, 3),
-        "latency_ms_pcie_inclusive": round(pcie_latency_ms, 3),
+        "latency_ms": round(pcie_latency_ms, 3),
+        "latency_ms_staged": round(ms_per_step, 3),
+        "latency_note": "latency_ms = one proof from a host witness (pinned-slot upload + proof + assembly), "
+                        "median of 5; latency_ms_staged = the timed loop's ms per proof, witness already in HBM",
+        "witness_upload": {"ms": round(upload_ms, 3), "bytes": wit_bytes,
+                           "host_GBps": round(wit_bytes / (upload_ms * 1e-3) / 1e9, 1) if upload_ms > 0 else None,
+                           "host_copy_threads": 4,
+                           "note": "pageable -> pinned host copies by 4 threads per upload overlapped with the "
+                                   "pinned -> HBM DMA; at 8 GPUs x proofs/s each this is the host's per-GPU load"},
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -587,6 +660,7 @@ def main():
         "stage_ms_last_proof": {k: round(v, 3) for k, v in stage_ms.items()},
         "batch_pcie_inclusive": batch,
         "roofline": roofline,
+        "roofline_launches": acc_lines,
     }
 
     if rehearsal:
@@ -602,12 +676,14 @@ def main():
         kb, kst, msm_case = kernel_benches(devices[0])
         out["kernels_config1"] = kb
         if peak and kst["ms_accumulate"] > 0:
-            # the same kernel alone on the GPU (configs[1] G1 MSM 2^20, uniform scalars): the in-proof
-            # average above is stretched by the three other streams sharing the CUs
+            # the same kernel alone on the GPU (configs[1] G1 MSM 2^20, uniform scalars)
             iso = kst["mixed_adds"] * FPMUL_PER_MADD * MAC_PER_FPMUL / (kst["ms_accumulate"] * 1e-3) / 1e12
             roofline["isolated_launch"] = {"workload": "configs[1] G1 MSM 2^20 accumulate, kernel alone",
                                            "mixed_adds": kst["mixed_adds"], "avg_launch_ms": round(kst["ms_accumulate"], 4),
                                            "achieved": round(iso, 3), "frac": round(iso / peak, 4)}
+    if args.bool0_line and args.bool_pct != 0 and args.scale == 1.0:
+        prover.close()  # its HBM goes to the all-uniform line's prover
+        out["all_uniform_witness"] = bool0_line(args, devices[0], R_FIX, S_FIX)
 
     if args.cpu_baseline == "full":
         out["cpu_baseline"] = cpu_baseline(args, zk, wit[0], results[0][0], R_FIX, S_FIX, msm_case)

@@ -270,6 +270,11 @@ zkp_status zkp_prove_partial_ext_staged(zkp_prover* p, int slot, const void* con
  * additions, [3] G1 tasks, [4..7] the same for G2.  Enabling resets the counters. */
 zkp_status zkp_prover_instrument(zkp_prover* p, int on);
 zkp_status zkp_prover_kernel_stats(const zkp_prover* p, double* out, int n);
+/* Every instrumented bucket-accumulate launch since zkp_prover_instrument(p, 1), in order: record i =
+ * out[3i .. 3i+2] = {kind, mixed additions, ms (HIP events on the launch's stream)}, kind 0 / 1 / 2 =
+ * the witness MSMs A / B1 / C (G1), 3 = the H MSM (G1), 4 = the witness MSM B2 (G2).  Writes at most
+ * max_records records; *n_records = the number held (up to 65536 per pipeline). */
+zkp_status zkp_prover_launch_stats(const zkp_prover* p, double* out, int max_records, int* n_records);
 /* MSM configuration chosen at load (device 0): [0] witness-MSM window bits c, [1] its
  * base-table depth T, [2] its bucket groups ceil(W/T), [3..5] the same for the H MSM,
  * [6] bytes of precomputed base tables per device. */

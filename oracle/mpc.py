@@ -255,6 +255,14 @@ def beacon(z, beacon_bytes: bytes, num_iterations_exp: int, name: str | None = N
 
 # ------------------------------------------------------------------ section 10 bytes
 
+def mpc_name_bytes(name: str) -> bytes:
+    """UTF-8 bytes of a contributor name as snarkjs writes them: name.substring(0, 64) counts
+    UTF-16 code units (a surrogate pair is two; a cut through one keeps its high half, which
+    TextEncoder writes as U+FFFD), then encodes; at most 192 bytes, below the 255 of the length byte."""
+    u16 = name.encode("utf-16-le")[:128]
+    return u16.decode("utf-16-le", errors="replace").encode("utf-8")
+
+
 def write_mpc(mpc) -> bytes:
     out = [mpc["cs_hash"], struct.pack("<I", len(mpc["contributions"]))]
     for c in mpc["contributions"]:
@@ -262,10 +270,10 @@ def write_mpc(mpc) -> bytes:
                 bn254.g2_to_lem(c["g2_spx"]), c["transcript"], struct.pack("<I", c.get("type", 0))]
         params = []
         if c.get("name") is not None:
-            nm = c["name"].encode("utf-8")[:64]
+            nm = mpc_name_bytes(c["name"])
             params += [1, len(nm)] + list(nm)
-        if c.get("type", 0) == 1:
-            params += [2, 1, c["numIterationsExp"], 3, len(c["beaconHash"])] + list(c["beaconHash"])
+        if c.get("type", 0) == 1:  # id 2 carries its one value byte directly (no length byte)
+            params += [2, c["numIterationsExp"], 3, len(c["beaconHash"])] + list(c["beaconHash"])
         out += [struct.pack("<I", len(params)), bytes(params)]
     return b"".join(out)
 
@@ -286,13 +294,18 @@ def read_mpc(sec: bytes):
         o += plen
         j = 0
         while j < len(prm):
-            pid, ln = prm[j], prm[j + 1]
+            pid = prm[j]
+            if pid == 2:  # numIterationsExp: one value byte, no length
+                c["numIterationsExp"] = prm[j + 1]
+                j += 2
+                continue
+            if pid not in (1, 3):
+                raise ValueError("zkey: MPC parameter %d not recognized" % pid)
+            ln = prm[j + 1]
             val = prm[j + 2:j + 2 + ln]
             if pid == 1:
                 c["name"] = val.decode("utf-8")
-            elif pid == 2:
-                c["numIterationsExp"] = val[0]
-            elif pid == 3:
+            else:
                 c["beaconHash"] = bytes(val)
             j += 2 + ln
         cons.append(c)

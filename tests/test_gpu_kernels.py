@@ -48,9 +48,13 @@ def _blob(pts, scal):
     return b"".join(bn254.g1_to_lem(p) for p in pts), b"".join(bn254.int_to_le(x) for x in scal)
 
 
-@pytest.mark.parametrize("dense", ["1", "0"])  # kernel-level default (dense, hand-written sort) and compacted
+def _plan(monkeypatch, dense):
+    monkeypatch.setenv("ZKP_MSM", "plan=" + ("dense" if dense in (1, "1") else "compact"))
+
+
+@pytest.mark.parametrize("dense", ["1", "0"])  # kernel-level default (dense plan) and the witness plan's variant
 def test_msm_g1_edge_distributions(monkeypatch, dense):
-    monkeypatch.setenv("ZKP_MSM_DENSE", dense)
+    _plan(monkeypatch, dense)
     pts = _pts(300, 99)
     cases = {
         "empty": ([], []),
@@ -69,10 +73,11 @@ def test_msm_g1_edge_distributions(monkeypatch, dense):
         assert got == want, name
 
 
-def test_msm_g1_bucket_binning(monkeypatch):
-    # the opt-in two-level counting-sort plan (ZKP_PLAN_SORT=bins): skewed (one bucket),
-    # uniform, sparse and multi-group inputs against the oracle
-    monkeypatch.setenv("ZKP_PLAN_SORT", "bins")
+@pytest.mark.parametrize("dense", ["1", "0"])
+def test_msm_g1_skewed_and_multigroup(monkeypatch, dense):
+    # skewed (one bucket), uniform, sparse and multi-group inputs on both plan variants: the
+    # wave-aggregated LDS claims and the tiled pass C (compact), one workgroup per sub-bin (dense)
+    _plan(monkeypatch, dense)
     pts = _pts(300, 41)
     rng = circuit.SplitMix64(42, 1)
     uni = [rng.fr() for _ in range(300)]
@@ -80,7 +85,7 @@ def test_msm_g1_bucket_binning(monkeypatch):
         (pts, uni, 0, 0),
         (pts, [1] * 150 + uni[:150], 0, 0),          # circuit-like: half the entries in bucket 0
         (pts, [1] * 300, 8, 0),
-        (pts, uni, 6, 4),                             # 2 bucket groups
+        (pts, uni, 8, 4),                             # 8 bucket groups
         (pts, [0] * 299 + [5], 0, 0),
         (pts[:1], [0], 0, 0),
     ]
@@ -90,10 +95,9 @@ def test_msm_g1_bucket_binning(monkeypatch):
 
 
 def test_msm_g1_dense_counting_sort(monkeypatch):
-    # the dense plan (every (window, point) digit an entry, zero digits dropped) grouped by the
-    # hand-written two-level counting sort (k_dsort_*): uniform, skewed (one bucket), sparse,
-    # degenerate, multi-group and every-window-bits inputs against the oracle
-    monkeypatch.setenv("ZKP_MSM_DENSE", "1")
+    # the dense plan grouped by the hand-written three-pass bucket sort: uniform, skewed (one
+    # bucket), sparse, degenerate, multi-group and every-window-bits inputs against the oracle
+    _plan(monkeypatch, 1)
     pts = _pts(300, 43)
     rng = circuit.SplitMix64(44, 1)
     uni = [rng.fr() for _ in range(300)]
@@ -102,7 +106,7 @@ def test_msm_g1_dense_counting_sort(monkeypatch):
         (pts, uni, 20, 0),                            # the H plan's window bits: 2^19 buckets, fine bits 10
         (pts, uni, 24, 0),                            # fine bits 14 (the largest LDS histogram)
         (pts, uni, 8, 0), (pts, uni, 9, 0),           # W = 32 / 29 windows: one scalar per thread per round
-        (pts, uni, 6, 4),                             # 2 bucket groups (bucket count not a power of two)
+        (pts, uni, 10, 4),                            # 7 bucket groups (bucket count not a power of two)
         (pts, [1] * 150 + uni[:150], 0, 0),           # half the entries in one bucket
         (pts, [1] * 300, 16, 0),
         ([pts[0]] * 300, list(range(1, 301)), 0, 0),  # doublings inside buckets
@@ -116,14 +120,11 @@ def test_msm_g1_dense_counting_sort(monkeypatch):
         assert zkp_amd.msm_g1(pb, sb, window_bits=c, table_depth=d) == groth16.msm_g1(p, [x % R for x in s]), (c, d)
 
 
-@pytest.mark.parametrize("balanced", [0, 1], ids=["uniform", "balanced"])
 @pytest.mark.parametrize("c", [17, 18, 19, 20, 21, 22])
-def test_msm_dense_window_bits(monkeypatch, c, balanced):
+def test_msm_dense_window_bits(monkeypatch, c):
     # the hand-written sort's bin / sub-bin / bucket bit splits of every window width around the
     # prover's choices (c = 18: 6 + 6 + 5 bits, 19: 7 + 6 + 5, 21: 8 + 7 + 5 ...), 2^15 uniform
-    # scalars over 64 bases: dense plan == compacted plan == the oracle's sum; with balanced window
-    # widths (ZKP_MSM_BALANCED=1: windows of c and c - 1 bits, the H plan's ZKP_H_BALANCED) too
-    monkeypatch.setenv("ZKP_MSM_BALANCED", str(balanced))
+    # scalars over 64 bases: dense plan == compacted plan == the oracle's sum
     rng = circuit.SplitMix64(46, 1)
     n = 1 << 15
     g = bn254.FixedBase(bn254.G1_GEN)
@@ -131,9 +132,9 @@ def test_msm_dense_window_bits(monkeypatch, c, balanced):
     pts = [base[i % 64] for i in range(n)]
     sc = [rng.fr() for _ in range(n)]
     pb, sb = _blob(pts, sc)
-    monkeypatch.setenv("ZKP_MSM_DENSE", "1")
+    _plan(monkeypatch, 1)
     got = zkp_amd.msm_g1(pb, sb, window_bits=c)
-    monkeypatch.setenv("ZKP_MSM_DENSE", "0")
+    _plan(monkeypatch, 0)
     assert zkp_amd.msm_g1(pb, sb, window_bits=c) == got
     acc = [0] * 64
     for i, x in enumerate(sc):
@@ -143,7 +144,8 @@ def test_msm_dense_window_bits(monkeypatch, c, balanced):
 
 def test_msm_dense_counting_sort_large(monkeypatch):
     # several scatter workgroups and every coarse bin populated: 2^14 uniform scalars at c = 20 on
-    # the dense plan vs the compacted plan (rocprim sort) of the same input, G1 and G2
+    # the dense plan vs the compacted plan of the same input; the subset sums (c = 20: 18 sums of
+    # 2^16 values) take the chain level below the trees, c = 13 the trees from the inputs
     rng = circuit.SplitMix64(45, 1)
     n = 1 << 14
     g = bn254.FixedBase(bn254.G1_GEN)
@@ -151,17 +153,11 @@ def test_msm_dense_counting_sort_large(monkeypatch):
     pts = [base[i % 64] for i in range(n)]
     sc = [rng.fr() for _ in range(n)]
     pb, sb = _blob(pts, sc)
-    monkeypatch.setenv("ZKP_MSM_DENSE", "0")
+    _plan(monkeypatch, 0)
     want = zkp_amd.msm_g1(pb, sb, window_bits=20)
-    monkeypatch.setenv("ZKP_MSM_DENSE", "1")
+    _plan(monkeypatch, 1)
     assert zkp_amd.msm_g1(pb, sb, window_bits=20) == want
     assert zkp_amd.msm_g1(pb, sb, window_bits=13) == want
-    # the subset sums (c = 20: 18 sums of 2^16 values) with a chain level below the trees (default
-    # above 512 workgroups), from the inputs by trees (two tree levels), and by the launch chain
-    monkeypatch.setenv("ZKP_TREE_FIRST_MAX", "100000")
-    assert zkp_amd.msm_g1(pb, sb, window_bits=20) == want
-    monkeypatch.setenv("ZKP_SUBSET_TREE", "0")
-    assert zkp_amd.msm_g1(pb, sb, window_bits=20) == want
     # the oracle on the same sum: scalars of equal bases add up
     acc = [0] * 64
     for i, x in enumerate(sc):
@@ -207,15 +203,25 @@ def test_quotient_golden(golden_dir, name):
 # Pippenger parameter variants: window bits c and base-table depth T (T = W: one shared
 # bucket set over precomputed 2^(c t) P rows; T = 1: one bucket group per window;
 # 1 < T < W: several groups folded by Horner with shift c*T).  Bit-exact vs the oracle.
+# (22, 2): 6 groups of 2^21 buckets = 24 key bits, the sort's 6-bit tiled pass C.
 @pytest.mark.parametrize("dense", ["1", "0"])
-@pytest.mark.parametrize("c,depth", [(0, 1), (5, 0), (5, 3), (8, 7), (13, 0), (2, 0), (20, 0)])
+@pytest.mark.parametrize("c,depth", [(0, 1), (8, 0), (8, 3), (9, 7), (13, 0), (20, 0), (24, 0), (22, 2)])
 def test_msm_g1_params(monkeypatch, c, depth, dense):
-    monkeypatch.setenv("ZKP_MSM_DENSE", dense)
+    _plan(monkeypatch, dense)
     pts = _pts(200, 5)
     rng = circuit.SplitMix64(6, 1)
     sc = [rng.fr() for _ in range(200)]
     pb, sb = _blob(pts, sc)
     assert zkp_amd.msm_g1(pb, sb, window_bits=c, table_depth=depth) == groth16.msm_g1(pts, sc)
+
+
+@pytest.mark.parametrize("c", [5, 25])
+def test_msm_window_bits_out_of_range(c):
+    pts = _pts(4, 5)
+    pb, sb = _blob(pts, [1, 2, 3, 4])
+    with pytest.raises(zkp_amd.ZkpError) as e:
+        zkp_amd.msm_g1(pb, sb, window_bits=c)
+    assert e.value.status == 1 and "window bits" in e.value.message
 
 
 def test_msm_g1_every_digit_one():
@@ -227,7 +233,7 @@ def test_msm_g1_every_digit_one():
     assert zkp_amd.msm_g1(pb, sb, window_bits=8) == groth16.msm_g1(pts, [s % R] * 200)
 
 
-@pytest.mark.parametrize("c,depth", [(0, 1), (6, 0), (6, 4)])
+@pytest.mark.parametrize("c,depth", [(0, 1), (8, 0), (8, 4)])
 def test_msm_g2_params(golden_dir, c, depth):
     n = 64
     pts, scal, exp = _load_msm(golden_dir, "msm_g2_%d.bin" % n, n, True)

@@ -32,18 +32,12 @@ def test_prove_bit_exact(golden_dir, name):
     assert groth16.js_stringify(res["publicSignals"]) == want_pub
 
 
-# plan / reduction / scheduling variants (read when the prover is built): the compacted H plan
-# instead of the dense one, the dense plan on the rocprim radix sort instead of the hand-written
-# counting sort, other bucket-reduction segment sizes and fan-ins, and the
-# scheduling gates, the subset sums by launch chains or with a chain level below the trees --
-# every variant must give the same golden proof
-KNOBS = [{"ZKP_H_DENSE": "0"}, {"ZKP_H_SORT": "rocprim"}, {"ZKP_TASK_ORDER": "bucket"}, {"ZKP_SEG_M": "16", "ZKP_SUB_L": "4"}, {"ZKP_SEG_M": "2", "ZKP_SUB_L": "16"},
-         {"ZKP_SCHED": "4"}, {"ZKP_SCHED": "5"}, {"ZKP_G2_FINISH_GATE": "1"}, {"ZKP_G2_FINISH_GATE": "2"},
-         {"ZKP_SUBSET_TREE": "0"}, {"ZKP_TREE_FIRST_MAX": "0"},
-         # round 3: balanced H-plan windows, the witness plan on rocprim / the low-priority stream,
-         # the tiled pass C for the H plan, the NTT roots staged per workgroup
-         {"ZKP_H_BALANCED": "1"}, {"ZKP_H_BALANCED": "0"}, {"ZKP_W_SORT": "rocprim"}, {"ZKP_WPLAN_HI": "0"},
-         {"ZKP_HS_TILED_C": "1"}, {"ZKP_NTT_RTAB": "0"}]
+# MSM tuning options (ZKP_MSM, read when the prover is built) and the serial profiling mode: other
+# window bits and table depths (several bucket groups folded by Horner), task sizes, bucket-reduction
+# segment sizes, every kernel alone on the device -- every variant must give the same golden proof
+KNOBS = [{"ZKP_MSM": "seg=16"}, {"ZKP_MSM": "seg=2"}, {"ZKP_MSM": "task_w=24,task_h=48"},
+         {"ZKP_MSM": "w=9,h=13"}, {"ZKP_MSM": "w=8,h=8,depth=3"}, {"ZKP_MSM": "w=20,h=20,depth=1"},
+         {"ZKP_SERIAL": "1"}]
 
 
 @pytest.mark.parametrize("knobs", KNOBS, ids=lambda k: ",".join("%s=%s" % kv for kv in k.items()))
@@ -92,6 +86,16 @@ def test_groth16_module_api(golden_dir, tmp_path):
     z = binfile.read_zkey(zk)
     assert groth16.verify_with_zkey(z, pub, groth16.proof_from_json_obj(pj))
     assert open(tmp_path / "public.json").read() == open(os.path.join(golden_dir, "public_tiny.json")).read()
+
+
+@pytest.mark.parametrize("spec", ["w=7", "h=25", "depth=0", "seg=3", "nope=1", "w"])
+def test_msm_options_rejected(golden_dir, monkeypatch, spec):
+    """A malformed ZKP_MSM option fails the load with ZKP_ERR_INVALID_ARG instead of tuning nothing."""
+    monkeypatch.setenv("ZKP_MSM", spec)
+    zk, _ = _files(golden_dir, "tiny")
+    with pytest.raises(zkp_amd.ZkpError) as e:
+        zkp_amd.Prover(zk)
+    assert e.value.status == 1 and ("ZKP_MSM" in e.value.message or "window bits" in e.value.message)
 
 
 def test_errors(golden_dir):
@@ -152,8 +156,7 @@ def test_batch_requeues_on_device_failure(golden_dir, monkeypatch):
     """Two pipelines (both on device 0); the test hook makes pipeline 1 report a device failure
     on its second proof: its witness is re-queued to pipeline 0, every proof of the batch
     succeeds bit-exactly, and later single proofs skip the failed pipeline."""
-    monkeypatch.setenv("ZKP_TEST_FAIL_PIPELINE", "1")
-    monkeypatch.setenv("ZKP_TEST_FAIL_AFTER", "1")
+    monkeypatch.setenv("ZKP_TEST_FAIL", "1:1")
     zk, wt = _files(golden_dir, "small")
     man = json.load(open(os.path.join(golden_dir, "manifest.json")))["circuits"]["small"]
     r, s = int(man["r"]), int(man["s"])

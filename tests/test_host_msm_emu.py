@@ -29,11 +29,11 @@ def emu(tmp_path_factory):
     return out
 
 
-def _run(emu, tmp_path, curve, pts, sc, c=0, d=0, bal=0):
+def _run(emu, tmp_path, curve, pts, sc, c=0, d=0):
     enc = bn254.g1_to_lem if curve == "g1" else bn254.g2_to_lem
     f = tmp_path / ("in_%s.bin" % curve)
     f.write_bytes(b"".join(enc(p) for p in pts) + b"".join(bn254.int_to_le(x) for x in sc))
-    out = subprocess.run([emu, curve, str(f), str(len(pts)), str(c), str(d), str(bal)], capture_output=True, text=True,
+    out = subprocess.run([emu, curve, str(f), str(len(pts)), str(c), str(d)], capture_output=True, text=True,
                          check=True, timeout=120).stdout.strip()
     if out == "inf":
         return None
@@ -47,18 +47,9 @@ PTS = [G1B.mul(rng.fr() or 1) for _ in range(64)]
 SC = [rng.fr() for _ in range(64)]
 
 
-@pytest.mark.parametrize("c,d", [(0, 0), (5, 3), (8, 0)])
+@pytest.mark.parametrize("c,d", [(0, 0), (8, 3), (8, 0), (13, 2)])
 def test_emu_g1_uniform(emu, tmp_path, c, d):
     assert _run(emu, tmp_path, "g1", PTS, SC, c, d) == groth16.msm_g1(PTS, SC)
-
-
-@pytest.mark.parametrize("c", [0, 6, 8, 13])
-def test_emu_g1_balanced_windows(emu, tmp_path, c):
-    """Balanced window widths (MsmParams::make(..., balanced): nb1 windows of c bits, the rest c - 1,
-    the H plan's ZKP_H_BALANCED): digits, the rows 2^(bit offset) P, scalars near r (top window)."""
-    assert _run(emu, tmp_path, "g1", PTS, SC, c, 0, 1) == groth16.msm_g1(PTS, SC)
-    top = [R - 1 - i for i in range(64)]
-    assert _run(emu, tmp_path, "g1", PTS, top, c, 0, 1) == groth16.msm_g1(PTS, top)
 
 
 def test_emu_g1_edge_pairs(emu, tmp_path):
@@ -76,14 +67,14 @@ def test_emu_g1_edge_pairs(emu, tmp_path):
     ]
     for pts, sc in cases:
         want = groth16.msm_g1(pts, [x % R for x in sc])
-        assert _run(emu, tmp_path, "g1", pts, sc, 4, 0) == want, (pts, sc)
+        assert _run(emu, tmp_path, "g1", pts, sc, 8, 0) == want, (pts, sc)
 
 
 def test_emu_g2_edges(emu, tmp_path):
     p2 = [bn254.g2_mul(bn254.G2_GEN, rng.fr() or 1) for _ in range(12)]
     s2 = [rng.fr() for _ in range(12)]
-    assert _run(emu, tmp_path, "g2", p2, s2, 6, 0) == groth16.msm_g2(p2, s2)
-    assert _run(emu, tmp_path, "g2", p2, s2, 6, 0, 1) == groth16.msm_g2(p2, s2)
+    assert _run(emu, tmp_path, "g2", p2, s2, 8, 0) == groth16.msm_g2(p2, s2)
+    assert _run(emu, tmp_path, "g2", p2, s2, 9, 4) == groth16.msm_g2(p2, s2)
     P = p2[0]
     for pts, sc in [([P, P], [1, 1]), ([P, bn254.g2_neg(P), p2[1]], [1, 1, 1]), ([None, P], [1, 1])]:
-        assert _run(emu, tmp_path, "g2", pts, sc, 4, 0) == groth16.msm_g2(pts, sc), (pts, sc)
+        assert _run(emu, tmp_path, "g2", pts, sc, 8, 0) == groth16.msm_g2(pts, sc), (pts, sc)

@@ -107,6 +107,36 @@ def test_node_mem_zkey_resident_and_release_while_in_flight():
     assert out["same"] and out["proof"] == json.load(open(os.path.join(GOLD, "proof_small.json")))
 
 
+@pytest.mark.gpu
+def test_node_mem_zkey_refilled_buffer_is_not_stale():
+    """the resident-prover cache is keyed by the buffer's content hash, computed once per
+    (ArrayBuffer, offset, length).  A buffer re-filled in place with another key of the same length
+    (here alpha1 <- beta1 in the header, so piA changes) must not reuse the first key's prover: the
+    sampled fingerprint checked on every hit catches it and the proof equals a fresh load's."""
+    from oracle import binfile
+    man = json.load(open(os.path.join(GOLD, "manifest.json")))["circuits"]["small"]
+    zk = os.path.join(GOLD, "circuit_small.zkey")
+    wt = os.path.join(GOLD, "circuit_small.wtns")
+    _, secs = binfile.read_binfile(open(zk, "rb").read(), b"zkey", 1)
+    h = secs[2][0][0]
+    alpha, beta = h + 84, h + 148
+    r = node("const fs=require('fs');const z=require('./zk-p2p-onramp_amd/js/groth16.js');"
+             "const buf=fs.readFileSync(%r), K={type:'mem',data:buf}, W={type:'mem',data:fs.readFileSync(%r)};"
+             "const o={r:%r,s:%r};"
+             "(async()=>{"
+             " const a=await z.groth16.prove(K,W,undefined,o);"
+             " buf.copy(buf, %d, %d, %d);"
+             " const b=await z.groth16.prove(K,W,undefined,o);"
+             " const c=await z.groth16.prove({type:'mem',data:Buffer.from(buf)},W,undefined,o);"
+             " console.log(JSON.stringify({differs:JSON.stringify(a.proof)!==JSON.stringify(b.proof),"
+             "  fresh:JSON.stringify(b.proof)===JSON.stringify(c.proof)}));"
+             "})().catch(e=>{console.log(JSON.stringify({err:e.message}));process.exit(1)})"
+             % (zk, wt, man["r"], man["s"], alpha, beta, beta + 64))
+    assert r.returncode == 0, r.stdout + r.stderr
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out == {"differs": True, "fresh": True}
+
+
 def test_addon_zkey_new_checks_arguments():
     r = node("const a=require('./zk-p2p-onramp_amd/js/build/zkp_napi.node');"
              "const z=require('./zk-p2p-onramp_amd/js/groth16.js');"

@@ -12,6 +12,7 @@ GPU: new -> contribute -> beacon through the C ABI is byte-identical to the orac
 final key passes `zkey verify` against the initial one and proves; the raw primitive
 (zkp_zkey_contribute, no record) is rejected."""
 import hashlib
+import struct
 import os
 
 import pytest
@@ -90,3 +91,27 @@ def test_gpu_ceremony_matches_oracle_and_verifies(name):
     assert not mpc.zkey_verify(bad, k0)[0]
     fresh = zkp_amd.zkey_contribute_entropy(k1, "other entropy")  # /dev/urandom: a different, valid key
     assert fresh != k2 and mpc.zkey_verify(fresh, k0)[0]
+
+
+def test_mpc_params_bytes_pinned():
+    """The contribution parameter bytes as snarkjs writeMPCParams lays them out: id 1
+    (name: length byte, UTF-8), id 2 (numIterationsExp: ONE value byte, no length byte), id 3
+    (beacon hash: length byte, bytes); the reader takes id 2's value byte directly."""
+    _, _, _, z1, z2 = _chain()
+    sec = mpc.write_mpc(z2.extra["mpc"])
+    nm = b"Final Beacon phase2"
+    want = bytes([1, len(nm)]) + nm + bytes([2, 10, 3, len(BEACON)]) + BEACON
+    assert sec.endswith(struct.pack("<I", len(want)) + want)
+    back = mpc.read_mpc(sec)["contributions"][-1]
+    assert back["numIterationsExp"] == 10 and back["beaconHash"] == BEACON and back["name"] == nm.decode()
+    first = mpc.write_mpc(z1.extra["mpc"])
+    nm1 = b"first contribution"
+    assert first.endswith(struct.pack("<I", 2 + len(nm1)) + bytes([1, len(nm1)]) + nm1)
+
+
+def test_mpc_name_truncation_utf16_units():
+    """snarkjs name.substring(0, 64) counts UTF-16 code units before UTF-8 encoding."""
+    assert mpc.mpc_name_bytes("a" * 70) == b"a" * 64
+    assert mpc.mpc_name_bytes("é" * 70) == "é".encode() * 64          # 2 UTF-8 bytes, 1 unit
+    assert mpc.mpc_name_bytes("\U0001F600" * 40) == "\U0001F600".encode() * 32  # 4 bytes, 2 units
+    assert mpc.mpc_name_bytes("a" + "\U0001F600" * 40) == b"a" + "\U0001F600".encode() * 31 + "�".encode()

@@ -59,16 +59,8 @@ def main(out=None, work="/tmp/zkp_coldstart"):
     buf, res["inflate_merge_parallel_s"] = timed(lambda: zkp_amd.read_zkey(chunk_path))
     assert buf == raw, "chunked key does not read back"
     del buf
-    os.environ["ZKP_IO_THREADS"] = "1"
-    buf, res["inflate_merge_1thread_s"] = timed(lambda: zkp_amd.read_zkey(chunk_path))
-    del buf
-    os.environ.pop("ZKP_IO_THREADS")
     p, res["load_chunks_gz_parallel_s"] = timed(lambda: zkp_amd.Prover(chunk_path, devices=[0]))
     p.close()
-    os.environ["ZKP_IO_THREADS"] = "1"
-    p, res["load_chunks_gz_1thread_s"] = timed(lambda: zkp_amd.Prover(chunk_path, devices=[0]))
-    p.close()
-    os.environ.pop("ZKP_IO_THREADS")
     p, res["load_plain_file_s"] = timed(lambda: zkp_amd.Prover(plain, devices=[0]))
     p.close()
     p, res["load_from_memory_s"] = timed(lambda: zkp_amd.Prover(zk, devices=[0]))

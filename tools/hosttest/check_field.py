@@ -123,18 +123,6 @@ def main(n=300):
         for b in [0, 4 * R, 3 * R - 1, rnd.randrange(3 * R)]:
             lines.append("sub4r %s %s" % (w8(a), w8(b)))
             checks.append(("sub4r", lambda z, a=a, b=b: z % R == (a - b) % R and z < 2 * R))
-    # NTT radix-4 unit (field.hpp r4_dif): inputs and roots < 2m, incl. all-extreme operands
-    r4 = [[rnd.randrange(2 * R) for _ in range(9)] for _ in range(n)]
-    r4 += [[2 * R - 1] * 9, [0] * 9, [2 * R - 1, 0, 0, 2 * R - 1] + [2 * R - 1] * 5,
-           [0, 2 * R - 1, 2 * R - 1, 0] + [2 * R - 1] * 5, [R, R - 1, 1, 2 * R - 1, 1, 2 * R - 1, 0, 1, R]]
-    for t in r4:
-        x0, x1, x2, x3, wa, wb, wc, wd, wj = t
-        lines.append("r4d %s" % " ".join(w8(x) for x in t))
-        u, v = x0 - x2, x1 - x3
-        checks.append(("r4d_y0", lambda z, t=x0 + x1 + x2 + x3: z % R == t % R and z < 2 * R))
-        checks.append(("r4d_y1", lambda z, t=(x0 + x2 - x1 - x3) * wj: z % R == t * inv_rp_r % R and z < 2 * R))
-        checks.append(("r4d_y2", lambda z, t=u * wa + v * wb: z % R == t * inv_rp_r % R and z < 2 * R))
-        checks.append(("r4d_y3", lambda z, t=u * wc + v * wd: z % R == t * inv_rp_r % R and z < 2 * R))
     # lazily reduced G1 accumulator x (field.hpp sub_2x8 / lsub8 / canon8, curve.hpp acc_*): a, b, c
     # < 2m give x < 8m; consumers mul, sqr(lsub8), mul2 with an unnormalised rsub operand
     x8 = [[rnd.randrange(2 * P) for _ in range(4)] for _ in range(n)]

@@ -52,13 +52,6 @@ int main() {
       for (int i = 0; i < NL; ++i) printf("%08x ", q.v[i]);
     }
     else if (o == "sub4r") { Fr a = rdf<FrCfg>(), b = rdf<FrCfg>(); prf(sub4(a, b)); }
-    else if (o == "r4d") {  // NTT radix-4 unit r4_dif: prints y0, y1, y2, y3
-      Fr x0 = rdf<FrCfg>(), x1 = rdf<FrCfg>(), x2 = rdf<FrCfg>(), x3 = rdf<FrCfg>();
-      Fr wa = rdf<FrCfg>(), wb = rdf<FrCfg>(), wc = rdf<FrCfg>(), wd = rdf<FrCfg>(), wj = rdf<FrCfg>();
-      Fr y0, y1, y2, y3;
-      r4_dif(x0, x1, x2, x3, wa, wb, wc, wd, wj, y0, y1, y2, y3);
-      prf(y0); printf("\n"); prf(y1); printf("\n"); prf(y2); printf("\n"); prf(y3);
-    }
     else if (o == "x8q") {  // lazily reduced accumulator x = a - b - 2c (< 8m) and its consumers
       Fq a = rdf<FqCfg>(), b = rdf<FqCfg>(), c = rdf<FqCfg>(), d = rdf<FqCfg>();
       const Fq x = sub_2x8(a, b, c);

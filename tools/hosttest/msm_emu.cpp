@@ -1,6 +1,6 @@
 // CPU replay of the MSM pipeline (msm_kernels.hpp per-thread bodies, same
 // parameters as MsmEngine) for debugging without a GPU.
-// usage: msm_emu <g1|g2> <file: points(zkey layout)|scalars> <n> [c] [depth] [balanced 0|1]   -> prints affine result (hex words)
+// usage: msm_emu <g1|g2> <file: points(zkey layout)|scalars> <n> [c] [depth]   -> prints affine result (decimal)
 #include <algorithm>
 #include <cstdio>
 #include <numeric>
@@ -11,7 +11,7 @@
 using namespace zkp;
 
 template <class F, class HF>
-static host::Jac<HF> run(std::vector<uint32_t>& pts, std::vector<uint32_t>& sc, uint32_t n, int c_ovr, int d_ovr, bool bal) {
+static host::Jac<HF> run(std::vector<uint32_t>& pts, std::vector<uint32_t>& sc, uint32_t n, int c_ovr, int d_ovr) {
   constexpr int FW = FWords<F>::W;
   // convert points to device layout
   for (size_t i = 0; i < pts.size() / 8; ++i) {
@@ -19,34 +19,37 @@ static host::Jac<HF> run(std::vector<uint32_t>& pts, std::vector<uint32_t>& sc, 
     x = mul(x, fe_const<FqCfg>(Conv::FQ_ZKEY_TO_DEV));
     store_fe(&pts[i * 8], x);
   }
-  MsmParams prm = MsmParams::make(std::max<uint32_t>(n, 1), c_ovr, d_ovr, bal);
+  MsmParams prm = MsmParams::make(std::max<uint32_t>(n, 1), c_ovr, d_ovr);
   const uint32_t W = prm.windows, T = prm.depth, G = prm.groups, half = 1u << (prm.c - 1), nb = G * half;
   // base table rows 1..T-1 (as MsmBases::extend)
   std::vector<uint32_t> table((size_t)T * n * 2 * FW);
   std::copy(pts.begin(), pts.begin() + (size_t)n * 2 * FW, table.begin());
   for (uint32_t t = 1; t < T; ++t)
-    for (uint32_t i = 0; i < n; ++i) msmk::extend_row<F>(i, table.data(), n, (int)t - 1 < prm.nb1 ? prm.c : prm.c - 1, (int)t);
-  // compacted digit emission (window-major, point order) as k_digit_count/k_digit_write
+    for (uint32_t i = 0; i < n; ++i) msmk::extend_row<F>(i, table.data(), n, prm.c, (int)t);
+  // the nonzero digits (window-major, point order); the device sort groups them by bucket in another order
   std::vector<std::vector<std::pair<uint32_t, uint32_t>>> per(W);
   for (uint32_t i = 0; i < n; ++i) {
     uint32_t s[9];
     msmk::load_scalar(sc.data(), i, s);
     uint32_t carry = 0, key, val;
     for (uint32_t w = 0; w < W; ++w)
-      if (msmk::digit_entry(s, (int)w, prm.c, prm.nb1, (int)T, n, i, carry, key, val)) per[w].push_back({key, val});
+      if (msmk::digit_entry(s, (int)w, prm.c, (int)T, n, i, carry, key, val)) per[w].push_back({key, val});
   }
   std::vector<uint32_t> ks, vs;
   for (auto& v : per)
     for (auto& e : v) ks.push_back(e.first), vs.push_back(e.second);
-  // stable sort on the bucket bits only (as the (c-1)-bit radix sort)
+  // stable sort on the whole bucket key (group and bucket bits), as the bucket sort groups them
   std::vector<uint32_t> idx(ks.size());
   std::iota(idx.begin(), idx.end(), 0);
-  std::stable_sort(idx.begin(), idx.end(), [&](uint32_t a, uint32_t b) { return (ks[a] & (half - 1)) < (ks[b] & (half - 1)); });
+  std::stable_sort(idx.begin(), idx.end(), [&](uint32_t a, uint32_t b) { return ks[a] < ks[b]; });
   { std::vector<uint32_t> k2(ks.size()), v2(ks.size()); for (size_t i = 0; i < idx.size(); ++i) { k2[i] = ks[idx[i]]; v2[i] = vs[idx[i]]; } ks.swap(k2); vs.swap(v2); }
   const uint32_t total2 = (uint32_t)ks.size();
   std::vector<uint32_t> st(nb + 1, 0), en(nb + 1, 0), cnt(nb + 1), off(nb + 1);
-  for (uint32_t i = 0; i < total2; ++i) msmk::bounds(i, ks.data(), total2, st.data(), en.data());
-  for (uint32_t b = 0; b <= nb; ++b) msmk::task_counts(b, st.data(), en.data(), nb, prm.S, cnt.data());
+  for (uint32_t i = 0; i < total2; ++i) {  // bucket [start, end) and ceil(len / S) tasks (as k_hs_fine / k_hs_bounds3)
+    if (i == 0 || ks[i - 1] != ks[i]) st[ks[i]] = i;
+    if (i == total2 - 1 || ks[i + 1] != ks[i]) en[ks[i]] = i + 1;
+  }
+  for (uint32_t b = 0; b <= nb; ++b) cnt[b] = b == nb ? 0u : (en[b] - st[b] + prm.S - 1) / prm.S;
   uint32_t acc = 0;
   for (uint32_t b = 0; b <= nb; ++b) { off[b] = acc; acc += cnt[b]; }
   const uint32_t ntask = off[nb];
@@ -66,19 +69,14 @@ static host::Jac<HF> run(std::vector<uint32_t>& pts, std::vector<uint32_t>& sc, 
   std::vector<uint32_t> buckets((size_t)nb * 4 * FW);
   for (uint32_t b = 0; b < nb; ++b)
     msmk::merge_final<F>(b, part.data(), part1.data(), off.data(), nb, prm.S2, levels, buckets.data());
-  // reduction (as run_engine): segments, subset sums, L-ary tree
-  const uint32_t M = prm.M, lgP = prm.lgP(), K = prm.K(), fan = prm.L, P = half / M;
+  // reduction (as run_finish): segments, then the K subset sums, each by one subset_first thread whose
+  // fan-in covers all its values (the device sums them by LDS trees: the same group elements)
+  const uint32_t M = prm.M, lgP = prm.lgP(), K = prm.K(), P = half / M, fan = std::max<uint32_t>(P, 1);
   std::vector<uint32_t> ss((size_t)G * P * 4 * FW), tt(ss.size());
   for (uint32_t id = 0; id < G * P; ++id) msmk::reduce_segments<F>(id, buckets.data(), G, half, M, ss.data(), tt.data());
-  uint32_t nn = msmk::subset_n1(lgP, fan);
-  std::vector<uint32_t> sub((size_t)G * K * nn * 4 * FW), sub2(sub.size());
+  const uint32_t nn = msmk::subset_n1(lgP, fan);  // 1
+  std::vector<uint32_t> sub((size_t)G * K * nn * 4 * FW);
   for (uint32_t id = 0; id < G * K * nn; ++id) msmk::subset_first<F>(id, ss.data(), tt.data(), G, lgP, fan, sub.data());
-  while (nn > 1) {
-    uint32_t next = (nn + fan - 1) / fan;
-    for (uint32_t id = 0; id < G * K * next; ++id) msmk::subset_level<F>(id, sub.data(), G * K, nn, fan, sub2.data());
-    std::swap(sub, sub2);
-    nn = next;
-  }
   // host fold (same as prover.hip msm_fold)
   auto ld = [&](uint32_t w) {
     const uint32_t* p = sub.data() + (size_t)w * 4 * FW;
@@ -108,18 +106,17 @@ int main(int argc, char** argv) {
   FILE* f = fopen(argv[2], "rb");
   uint32_t n = atoi(argv[3]);
   const int c_ovr = argc > 4 ? atoi(argv[4]) : 0, d_ovr = argc > 5 ? atoi(argv[5]) : 0;
-  const bool bal = argc > 6 && atoi(argv[6]) == 1;  // balanced window widths
   size_t pw = g2 ? 32 : 16;
   std::vector<uint32_t> pts(n * pw), sc(n * 8 + 8);
   if (fread(pts.data(), 4, pts.size(), f) != pts.size()) return 1;
   if (fread(sc.data(), 4, n * 8, f) != n * 8) return 1;
   if (!g2) {
-    auto a = host::jac_to_aff(run<Fq, host::Fq>(pts, sc, n, c_ovr, d_ovr, bal));
+    auto a = host::jac_to_aff(run<Fq, host::Fq>(pts, sc, n, c_ovr, d_ovr));
     if (a.inf) { printf("inf\n"); return 0; }
     auto x = a.x.to_std(), y = a.y.to_std();
     printf("%s %s\n", host::u256_to_dec(x).c_str(), host::u256_to_dec(y).c_str());
   } else {
-    auto a = host::jac_to_aff(run<Fq2, host::Fq2>(pts, sc, n, c_ovr, d_ovr, bal));
+    auto a = host::jac_to_aff(run<Fq2, host::Fq2>(pts, sc, n, c_ovr, d_ovr));
     if (a.inf) { printf("inf\n"); return 0; }
     printf("%s %s %s %s\n", host::u256_to_dec(a.x.c0.to_std()).c_str(), host::u256_to_dec(a.x.c1.to_std()).c_str(),
            host::u256_to_dec(a.y.c0.to_std()).c_str(), host::u256_to_dec(a.y.c1.to_std()).c_str());

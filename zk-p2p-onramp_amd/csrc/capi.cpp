@@ -1,5 +1,6 @@
 // C ABI of libzkp_amd.so (include/zkp_amd.h).  Every entry point catches all C++
 // exceptions and turns them into a zkp_status plus a thread-local message.
+#include <stdexcept>
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -48,6 +49,8 @@ zkp_status guard(Fn&& fn) {
     return fail(ZKP_ERR_DEVICE, e.what());
   } catch (const std::bad_alloc&) {
     return fail(ZKP_ERR_OUT_OF_MEMORY, "host out of memory");
+  } catch (const std::invalid_argument& e) {
+    return fail(ZKP_ERR_INVALID_ARG, e.what());
   } catch (const std::exception& e) {
     return fail(ZKP_ERR_INTERNAL, e.what());
   } catch (...) {
@@ -531,6 +534,11 @@ zkp_status zkp_prover_instrument(zkp_prover* p, int on) {
 zkp_status zkp_prover_kernel_stats(const zkp_prover* p, double* out, int n) {
   if (!p || !out) return fail(ZKP_ERR_INVALID_ARG, "null argument");
   return guard([&] { p->impl->kernel_stats(out, n); });
+}
+
+zkp_status zkp_prover_launch_stats(const zkp_prover* p, double* out, int max_records, int* n_records) {
+  if (!p || !n_records || (max_records > 0 && !out)) return fail(ZKP_ERR_INVALID_ARG, "null argument");
+  return guard([&] { *n_records = p->impl->launch_records(out, max_records); });
 }
 
 zkp_status zkp_bench_msm(int device, int g2, const uint8_t* points, const uint8_t* scalars, size_t n, int warmup,

@@ -74,12 +74,9 @@ template <class C>
 ZDEV Fe<C> acc_xcanon(const Fe<C>& x) { return canon8(x); }
 ZDEV Fq2 acc_xcanon(const Fq2& x) { return canon4(x); }
 
-// independent products of the mixed addition in lockstep (ZKP_MUL_PAIRS: 0 off, 1 pairs, 2 pairs +
-// a triple): a chained field config (C::CHAIN) runs each group with interleaved column chains
-// (field.hpp mul_pair / sqr_pair / mul_triple / mul_mul2_pair); otherwise, and for Fq2, plain products
-#ifndef ZKP_MUL_PAIRS
-#define ZKP_MUL_PAIRS 1  // 2 measured: in-proof launches slower, isolated faster, proof +0.1 ms (profiles/mul_pairs_r03.txt)
-#endif
+// independent products of the mixed addition in lockstep: a chained field config (C::CHAIN) runs
+// each pair with interleaved column chains (field.hpp mul_pair / sqr_pair); otherwise, and for Fq2,
+// plain products (a lockstep triple measured no better, profiles/mul_pairs_r03.txt)
 template <class F>
 ZDEV void mul_2(const F& a, const F& b, const F& c, const F& d, F& r, F& s) {
   r = mul(a, b);
@@ -87,43 +84,11 @@ ZDEV void mul_2(const F& a, const F& b, const F& c, const F& d, F& r, F& s) {
 }
 template <class C>
 ZDEV void mul_2(const Fe<C>& a, const Fe<C>& b, const Fe<C>& c, const Fe<C>& d, Fe<C>& r, Fe<C>& s) {
-  if constexpr (C::CHAIN && ZKP_MUL_PAIRS) {
+  if constexpr (C::CHAIN) {
     mul_pair(a, b, c, d, r, s);
   } else {
     r = mul(a, b);
     s = mul(c, d);
-  }
-}
-// PPP = P PP, Q = X1 PP, ZZ3 = ZZ1 PP (triple), then ZZZ3 = ZZZ1 PPP beside the Y3 sum of
-// products (ZKP_MUL_PAIRS=2): the mixed addition's last products without lone chains
-template <class F>
-ZDEV void mul_3(const F& a, const F& b, const F& c, const F& d, const F& e, const F& f, F& r, F& s, F& t) {
-  mul_2(a, b, c, d, r, s);
-  t = mul(e, f);
-}
-template <class C>
-ZDEV void mul_3(const Fe<C>& a, const Fe<C>& b, const Fe<C>& c, const Fe<C>& d, const Fe<C>& e, const Fe<C>& f,
-                Fe<C>& r, Fe<C>& s, Fe<C>& t) {
-  if constexpr (C::CHAIN && ZKP_MUL_PAIRS >= 2) {
-    mul_triple(a, b, c, d, e, f, r, s, t);
-  } else {
-    mul_2(a, b, c, d, r, s);
-    t = mul(e, f);
-  }
-}
-template <class F>
-ZDEV void mul_y3_2(const F& a, const F& b, const F& r, const F& t, const F& y, const F& d, F& zzz, F& y3) {
-  zzz = mul(a, b);
-  y3 = acc_y3(r, t, y, d);
-}
-template <class C>
-ZDEV void mul_y3_2(const Fe<C>& a, const Fe<C>& b, const Fe<C>& r, const Fe<C>& t, const Fe<C>& y, const Fe<C>& d,
-                   Fe<C>& zzz, Fe<C>& y3) {
-  if constexpr (C::CHAIN && ZKP_MUL_PAIRS >= 2) {
-    mul_mul2_pair(a, b, r, t, y, d, zzz, y3);  // y3 = r t + y d, as acc_y3
-  } else {
-    zzz = mul(a, b);
-    y3 = acc_y3(r, t, y, d);
   }
 }
 template <class F>
@@ -133,7 +98,7 @@ ZDEV void acc_sqr_2(const F& a, const F& c, F& r, F& s) {
 }
 template <class C>
 ZDEV void acc_sqr_2(const Fe<C>& a, const Fe<C>& c, Fe<C>& r, Fe<C>& s) {
-  if constexpr (C::CHAIN && ZKP_MUL_PAIRS) {
+  if constexpr (C::CHAIN) {
     sqr_pair(a, c, r, s);
   } else {
     r = acc_sqr(a);
@@ -250,19 +215,12 @@ ZDEV void xyzz_add_aff(Xyzz<F>& acc, const Aff<F>& q, bool neg = false) {
       return;
     }
   }
-  F PPP, Q, ZZ3, ZZZ3, Y3;
-  if (ZKP_MUL_PAIRS >= 2) {
-    mul_3(P, PP, acc.x, PP, acc.zz, PP, PPP, Q, ZZ3);
-    const F X3 = acc_x3(RR, PPP, Q);
-    mul_y3_2(acc.zzz, PPP, R, acc_xsub(Q, X3), acc.y, acc_negd(PPP), ZZZ3, Y3);  // Y3 = R (Q - X3) - Y1 PPP
-    acc.x = X3;
-  } else {
-    mul_2(P, PP, acc.x, PP, PPP, Q);
-    const F X3 = acc_x3(RR, PPP, Q);
-    Y3 = acc_y3(R, acc_xsub(Q, X3), acc.y, acc_negd(PPP));  // R (Q - X3) - Y1 PPP
-    mul_2(acc.zz, PP, acc.zzz, PPP, ZZ3, ZZZ3);
-    acc.x = X3;
-  }
+  F PPP, Q, ZZ3, ZZZ3;
+  mul_2(P, PP, acc.x, PP, PPP, Q);
+  const F X3 = acc_x3(RR, PPP, Q);
+  const F Y3 = acc_y3(R, acc_xsub(Q, X3), acc.y, acc_negd(PPP));  // R (Q - X3) - Y1 PPP
+  mul_2(acc.zz, PP, acc.zzz, PPP, ZZ3, ZZZ3);
+  acc.x = X3;
   acc.zz = ZZ3;
   acc.zzz = ZZZ3;
   acc.y = Y3;

@@ -39,42 +39,24 @@ using Fr = Fe<FrCfg>;
 
 // acc += x * y.  CH (C::CHAIN, device code): every product column stays ONE dependent chain seeded
 // by the previous column's carry.  Left to itself the compiler re-associates each column into a sum
-// from 0 plus a 64-bit join of the carry (v_lshl_add_u64 per column).  ZKP_MAC_FORM 2 (default):
-// after each product the accumulator passes through an EMPTY asm statement that claims to modify
-// it, so the column cannot be re-associated while the compiler still sees, schedules and
-// hazard-checks real v_mad_u64_u32 instructions (it interleaves independent products' chains to
-// cover the wait states between dependent 64-bit mads); 1: the mad itself as inline asm (the
-// compiler then pads every one with s_nop); 0: no chains.  tools/ubench/mul_chain.hip,
-// profiles/mul_chain_r03.txt.  mac_k takes a constant.  Host code is always plain C.
-#ifndef ZKP_MAC_FORM
-#define ZKP_MAC_FORM 2
-#endif
+// from 0 plus a 64-bit join of the carry (v_lshl_add_u64 per column).  After each product the
+// accumulator passes through an EMPTY asm statement that claims to modify it, so the column cannot be
+// re-associated while the compiler still sees, schedules and hazard-checks real v_mad_u64_u32
+// instructions (it interleaves independent products' chains to cover the wait states between
+// dependent 64-bit mads).  tools/ubench/mul_chain.hip, profiles/mul_chain_r03.txt.  mac_k takes a
+// constant.  Host code is always plain C.
 template <bool CH>
 ZDEV void mac(uint64_t& acc, uint32_t x, uint32_t y) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  if constexpr (CH && ZKP_MAC_FORM == 1) {
-    uint64_t cc;
-    asm("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc), "=s"(cc) : "v"(x), "v"(y));
-    return;
-  }
-#endif
   acc += (uint64_t)x * y;
 #if defined(__HIP_DEVICE_COMPILE__)
-  if constexpr (CH && ZKP_MAC_FORM == 2) asm("" : "+v"(acc));
+  if constexpr (CH) asm("" : "+v"(acc));
 #endif
 }
 template <bool CH>
 ZDEV void mac_k(uint64_t& acc, uint32_t x, uint32_t k) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  if constexpr (CH && ZKP_MAC_FORM == 1) {
-    uint64_t cc;
-    asm("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc), "=s"(cc) : "v"(x), "s"(k));
-    return;
-  }
-#endif
   acc += (uint64_t)x * k;
 #if defined(__HIP_DEVICE_COMPILE__)
-  if constexpr (CH && ZKP_MAC_FORM == 2) asm("" : "+v"(acc));
+  if constexpr (CH) asm("" : "+v"(acc));
 #endif
 }
 
@@ -269,50 +251,6 @@ ZDEV Fe<C> mul2(const Fe<C>& a, const Fe<C>& b, const Fe<C>& c, const Fe<C>& d) 
   return r;
 }
 
-// (a*b + c*d + e*f + g*h)/2^261 mod m with one reduction: columns hold <= 36 + 9 partial
-// products < 2^58 (< 2^63.5).  All operands normalised, the sum < ~169 m^2.  Fq2 sums of
-// products (Y3 of the G2 additions).
-template <class C>
-ZDEV Fe<C> mul4(const Fe<C>& a, const Fe<C>& b, const Fe<C>& c, const Fe<C>& d, const Fe<C>& e, const Fe<C>& f,
-                const Fe<C>& g, const Fe<C>& h) {
-  uint32_t m[NL];
-  Fe<C> r;
-  uint64_t acc = 0;
-#pragma unroll
-  for (int i = 0; i < NL; ++i) {
-#pragma unroll
-    for (int j = 0; j < i; ++j) {
-      mac<C::CHAIN>(acc, a.v[j], b.v[i - j]);
-      mac<C::CHAIN>(acc, c.v[j], d.v[i - j]);
-      mac<C::CHAIN>(acc, e.v[j], f.v[i - j]);
-      mac<C::CHAIN>(acc, g.v[j], h.v[i - j]);
-      mac_k<C::CHAIN>(acc, m[j], C::MOD[i - j]);
-    }
-    mac<C::CHAIN>(acc, a.v[i], b.v[0]);
-    mac<C::CHAIN>(acc, c.v[i], d.v[0]);
-    mac<C::CHAIN>(acc, e.v[i], f.v[0]);
-    mac<C::CHAIN>(acc, g.v[i], h.v[0]);
-    m[i] = ((uint32_t)acc * C::INV) & LMASK;
-    mac_k<C::CHAIN>(acc, m[i], C::MOD[0]);
-    acc >>= LB;
-  }
-#pragma unroll
-  for (int i = NL; i < 2 * NL - 1; ++i) {
-#pragma unroll
-    for (int j = i - NL + 1; j < NL; ++j) {
-      mac<C::CHAIN>(acc, a.v[j], b.v[i - j]);
-      mac<C::CHAIN>(acc, c.v[j], d.v[i - j]);
-      mac<C::CHAIN>(acc, e.v[j], f.v[i - j]);
-      mac<C::CHAIN>(acc, g.v[j], h.v[i - j]);
-      mac_k<C::CHAIN>(acc, m[j], C::MOD[i - j]);
-    }
-    r.v[i - NL] = (uint32_t)acc & LMASK;
-    acc >>= LB;
-  }
-  r.v[NL - 1] = (uint32_t)acc;
-  return r;
-}
-
 // Squaring: cross products computed once against a doubled operand.
 template <class C>
 ZDEV Fe<C> sqr(const Fe<C>& a) {
@@ -389,9 +327,10 @@ ZDEV void mul_pair(const Fe<C>& a, const Fe<C>& b, const Fe<C>& c, const Fe<C>& 
   s.v[NL - 1] = (uint32_t)y;
 }
 
-// Two lazily reduced sums of N products, r = sum_k a[k] b[k], s = sum_k c[k] d[k] (mul2 / mul4 each),
-// in lockstep with chained columns when CH: the Fq2 products of the G2 arithmetic (c0 and c1 of a
-// product, ZKP_CHAIN_G2).  Operand conditions as mul2 / mul4.
+// Two lazily reduced sums of N products, r = sum_k a[k] b[k], s = sum_k c[k] d[k], in lockstep with
+// chained columns when CH: the Fq2 products of the G2 arithmetic (c0 and c1 of a product).  Operand
+// conditions as mul2; N = 4: columns hold <= 36 + 9 partial products < 2^58 (< 2^63.5), the sum
+// < ~169 m^2.
 template <class C, bool CH, int N>
 ZDEV void sop_pair(const Fe<C>* const (&a)[N], const Fe<C>* const (&b)[N], const Fe<C>* const (&c)[N],
                    const Fe<C>* const (&d)[N], Fe<C>& r, Fe<C>& s) {
@@ -432,104 +371,6 @@ ZDEV void sop_pair(const Fe<C>* const (&a)[N], const Fe<C>* const (&b)[N], const
       }
       mac_k<CH>(x, m[j], C::MOD[i - j]);
       mac_k<CH>(y, n[j], C::MOD[i - j]);
-    }
-    r.v[i - NL] = (uint32_t)x & LMASK;
-    s.v[i - NL] = (uint32_t)y & LMASK;
-    x >>= LB;
-    y >>= LB;
-  }
-  r.v[NL - 1] = (uint32_t)x;
-  s.v[NL - 1] = (uint32_t)y;
-}
-
-// three independent products in lockstep (two other mads between dependent ones of a chain)
-template <class C>
-ZDEV void mul_triple(const Fe<C>& a, const Fe<C>& b, const Fe<C>& c, const Fe<C>& d, const Fe<C>& e, const Fe<C>& f,
-                     Fe<C>& r, Fe<C>& s, Fe<C>& t) {
-  uint32_t m[NL], n[NL], o[NL];
-  uint64_t x = 0, y = 0, z = 0;
-#pragma unroll
-  for (int i = 0; i < NL; ++i) {
-#pragma unroll
-    for (int j = 0; j < i; ++j) {
-      mac<C::CHAIN>(x, a.v[j], b.v[i - j]);
-      mac<C::CHAIN>(y, c.v[j], d.v[i - j]);
-      mac<C::CHAIN>(z, e.v[j], f.v[i - j]);
-      mac_k<C::CHAIN>(x, m[j], C::MOD[i - j]);
-      mac_k<C::CHAIN>(y, n[j], C::MOD[i - j]);
-      mac_k<C::CHAIN>(z, o[j], C::MOD[i - j]);
-    }
-    mac<C::CHAIN>(x, a.v[i], b.v[0]);
-    mac<C::CHAIN>(y, c.v[i], d.v[0]);
-    mac<C::CHAIN>(z, e.v[i], f.v[0]);
-    m[i] = ((uint32_t)x * C::INV) & LMASK;
-    n[i] = ((uint32_t)y * C::INV) & LMASK;
-    o[i] = ((uint32_t)z * C::INV) & LMASK;
-    mac_k<C::CHAIN>(x, m[i], C::MOD[0]);
-    mac_k<C::CHAIN>(y, n[i], C::MOD[0]);
-    mac_k<C::CHAIN>(z, o[i], C::MOD[0]);
-    x >>= LB;
-    y >>= LB;
-    z >>= LB;
-  }
-#pragma unroll
-  for (int i = NL; i < 2 * NL - 1; ++i) {
-#pragma unroll
-    for (int j = i - NL + 1; j < NL; ++j) {
-      mac<C::CHAIN>(x, a.v[j], b.v[i - j]);
-      mac<C::CHAIN>(y, c.v[j], d.v[i - j]);
-      mac<C::CHAIN>(z, e.v[j], f.v[i - j]);
-      mac_k<C::CHAIN>(x, m[j], C::MOD[i - j]);
-      mac_k<C::CHAIN>(y, n[j], C::MOD[i - j]);
-      mac_k<C::CHAIN>(z, o[j], C::MOD[i - j]);
-    }
-    r.v[i - NL] = (uint32_t)x & LMASK;
-    s.v[i - NL] = (uint32_t)y & LMASK;
-    t.v[i - NL] = (uint32_t)z & LMASK;
-    x >>= LB;
-    y >>= LB;
-    z >>= LB;
-  }
-  r.v[NL - 1] = (uint32_t)x;
-  s.v[NL - 1] = (uint32_t)y;
-  t.v[NL - 1] = (uint32_t)z;
-}
-
-// a product and a lazily reduced sum of two products (mul2) in lockstep
-template <class C>
-ZDEV void mul_mul2_pair(const Fe<C>& a, const Fe<C>& b, const Fe<C>& c, const Fe<C>& d, const Fe<C>& e,
-                        const Fe<C>& f, Fe<C>& r, Fe<C>& s) {
-  uint32_t m[NL], n[NL];
-  uint64_t x = 0, y = 0;
-#pragma unroll
-  for (int i = 0; i < NL; ++i) {
-#pragma unroll
-    for (int j = 0; j < i; ++j) {
-      mac<C::CHAIN>(y, c.v[j], d.v[i - j]);
-      mac<C::CHAIN>(x, a.v[j], b.v[i - j]);
-      mac<C::CHAIN>(y, e.v[j], f.v[i - j]);
-      mac_k<C::CHAIN>(x, m[j], C::MOD[i - j]);
-      mac_k<C::CHAIN>(y, n[j], C::MOD[i - j]);
-    }
-    mac<C::CHAIN>(y, c.v[i], d.v[0]);
-    mac<C::CHAIN>(x, a.v[i], b.v[0]);
-    mac<C::CHAIN>(y, e.v[i], f.v[0]);
-    m[i] = ((uint32_t)x * C::INV) & LMASK;
-    n[i] = ((uint32_t)y * C::INV) & LMASK;
-    mac_k<C::CHAIN>(x, m[i], C::MOD[0]);
-    mac_k<C::CHAIN>(y, n[i], C::MOD[0]);
-    x >>= LB;
-    y >>= LB;
-  }
-#pragma unroll
-  for (int i = NL; i < 2 * NL - 1; ++i) {
-#pragma unroll
-    for (int j = i - NL + 1; j < NL; ++j) {
-      mac<C::CHAIN>(y, c.v[j], d.v[i - j]);
-      mac<C::CHAIN>(x, a.v[j], b.v[i - j]);
-      mac<C::CHAIN>(y, e.v[j], f.v[i - j]);
-      mac_k<C::CHAIN>(x, m[j], C::MOD[i - j]);
-      mac_k<C::CHAIN>(y, n[j], C::MOD[i - j]);
     }
     r.v[i - NL] = (uint32_t)x & LMASK;
     s.v[i - NL] = (uint32_t)y & LMASK;
@@ -830,26 +671,6 @@ ZDEV Fe<C> add_raw(const Fe<C>& a, const Fe<C>& b) {
   return s;
 }
 
-// DIF radix-4 unit (NTT stage pair) on normalised inputs < 2m and roots < 2m:
-//   y0 = s02 + s13, y1 = (s02 - s13) wj          (s02 = x0 + x2, s13 = x1 + x3 raw, < 4m)
-//   y2 = u wa + v wb, y3 = u wc + v wd           (u = x0 - x2, v = x1 - x3)
-// i.e. y2 = d02 + d13, y3 = (d02 - d13) wj for d02 = u wa, d13 = v wb with the combined roots
-// wc = wa wj, wd = -wb wj: each of y2, y3 is one lazily reduced sum of products (mul2), so the
-// unit takes 3 Montgomery reductions instead of 4 and no addition of products.  u = x0 - x2 + 4m
-// is raw (limbs < 2^31, < 6m) beside a normalised root, v = x1 - x3 + 2m normalised (< 4m): the
-// mul2 column sums stay < 9*2^60 + 18*2^58 < 2^64, u wa + v wb < 20 m^2 (output < 2m).
-template <class C>
-ZDEV void r4_dif(const Fe<C>& x0, const Fe<C>& x1, const Fe<C>& x2, const Fe<C>& x3, const Fe<C>& wa,
-                 const Fe<C>& wb, const Fe<C>& wc, const Fe<C>& wd, const Fe<C>& wj, Fe<C>& y0, Fe<C>& y1,
-                 Fe<C>& y2, Fe<C>& y3) {
-  const Fe<C> s02 = add_raw(x0, x2), s13 = add_raw(x1, x3);
-  const Fe<C> u = rsub(x0, x2), v = lsub(x1, x3);
-  y0 = add_raw_reduce(s02, s13);
-  y1 = mul(sub_raw6(s02, s13), wj);
-  y2 = mul2(u, wa, v, wb);
-  y3 = mul2(u, wc, v, wd);
-}
-
 template <class C>
 ZDEV Fe<C> dbl(const Fe<C>& a) { return add(a, a); }
 
@@ -974,39 +795,26 @@ ZDEV Fq neg4(const Fq& a) {
 // (a0 + a1 u)(b0 + b1 u) = (a0 b0 - a1 b1) + (a0 b1 + a1 b0) u as two lazily reduced sums
 // of products (2 x 162 + 2 x 81 mads, like Karatsuba's 3 x 162, but no Karatsuba adds and
 // subtractions: ~650 instead of ~1100 instructions).  Components normalised, < 4m.
-// ZKP_CHAIN_G2 (default on): the two components' sums of products run in lockstep with chained
-// columns (sop_pair); 0: two independent mul2 / mul4 as the compiler schedules them
-#ifndef ZKP_CHAIN_G2
-#define ZKP_CHAIN_G2 1
-#endif
+// The two components' sums of products run in lockstep with chained columns (sop_pair): the 2-wave
+// G2 kernels gain with paired chains (profiles/g2_chain_r03.txt).
 ZDEV Fq2 mul(const Fq2& a, const Fq2& b) {
   Fq2 r;
-#if ZKP_CHAIN_G2
   const Fq nb1 = neg4(b.c1);
   const Fq* x0[2] = {&a.c0, &a.c1};
   const Fq* y0[2] = {&b.c0, &nb1};
   const Fq* y1[2] = {&b.c1, &b.c0};
   sop_pair<FqCfg, true, 2>(x0, y0, x0, y1, r.c0, r.c1);
-#else
-  r.c0 = mul2(a.c0, b.c0, a.c1, neg4(b.c1));
-  r.c1 = mul2(a.c0, b.c1, a.c1, b.c0);
-#endif
   return r;
 }
 
 // a*b + c*d in Fq2 with two lazily reduced four-product sums
 ZDEV Fq2 mul2(const Fq2& a, const Fq2& b, const Fq2& c, const Fq2& d) {
   Fq2 r;
-#if ZKP_CHAIN_G2
   const Fq nb1 = neg4(b.c1), nd1 = neg4(d.c1);
   const Fq* x[4] = {&a.c0, &a.c1, &c.c0, &c.c1};
   const Fq* y0[4] = {&b.c0, &nb1, &d.c0, &nd1};
   const Fq* y1[4] = {&b.c1, &b.c0, &d.c1, &d.c0};
   sop_pair<FqCfg, true, 4>(x, y0, x, y1, r.c0, r.c1);
-#else
-  r.c0 = mul4(a.c0, b.c0, a.c1, neg4(b.c1), c.c0, d.c0, c.c1, neg4(d.c1));
-  r.c1 = mul4(a.c0, b.c1, a.c1, b.c0, c.c0, d.c1, c.c1, d.c0);
-#endif
   return r;
 }
 
@@ -1029,7 +837,6 @@ ZDEV Fq2 lsub4_lazy(const Fq2& a, const Fq2& b) { return Fq2{lsub4(a.c0, b.c0), 
 // a^2 for components < 6m: (a0 + a1)(a0 - a1 + 6m) [raw sum x normalised, < 144 m^2] and
 // (2 a0) a1 [raw x normalised, < 72 m^2] -- no additions reduced, no doubling of the product
 ZDEV Fq2 sqr_lazy(const Fq2& a) {
-#if ZKP_CHAIN_G2
   const Fq s = add_raw(a.c0, a.c1), d = lsub6(a.c0, a.c1), t = shl1_raw(a.c0);
   const Fq* x0[1] = {&s};
   const Fq* y0[1] = {&d};
@@ -1038,9 +845,6 @@ ZDEV Fq2 sqr_lazy(const Fq2& a) {
   Fq2 r;
   sop_pair<FqCfg, true, 1>(x0, y0, x1, y1, r.c0, r.c1);
   return r;
-#else
-  return Fq2{mul(add_raw(a.c0, a.c1), lsub6(a.c0, a.c1)), mul(shl1_raw(a.c0), a.c1)};
-#endif
 }
 // R^2 - PPP - 2Q per component (each < 2m) -> < 4m: one conditional subtraction instead of two.
 // (Not qreduce: its single 27-deep dependent chain per component measured 6 % slower in the

@@ -1,11 +1,12 @@
-// Bucket sort of a dense MSM plan (the H MSM's uniform quotient scalars), hand-written for
-// gfx950, included by msm.hip.  It groups the n*W (window, point) digits by bucket key for the
-// accumulate tasks -- what rocprim's onesweep radix sort did before, whose decoupled look-back
-// stalls whenever the blocks it waits on share the CUs with the long accumulation kernels of the
-// other streams.  Here no workgroup ever waits on another one: every pass is reduce-then-scan.
+// Bucket sort of an MSM plan (the H MSM's uniform quotient scalars and the witness MSMs' 0/1-heavy
+// ones), hand-written for gfx950, included by msm.hip.  It groups the nonzero (window, point) digits
+// by bucket key for the accumulate tasks.  No workgroup ever waits on another one: every pass is
+// reduce-then-scan (a decoupled look-back radix sort, rocprim's onesweep, stalled whenever the blocks
+// it waits on shared the CUs with the long accumulation kernels of the other streams:
+// profiles/plan_sort_r02.json).
 //
 // Key bits kb = ceil(log2 buckets) split as b1 (bin) + b2 (sub-bin) + b3 (bucket in sub-bin);
-// for the Venmo H plan (2^19 buckets) 7 + 7 + 5.  Three MSD passes, every scatter staged in LDS
+// for the Venmo H plan (2^19 buckets) 7 + 7 + 5; b3 grows past 5 (tiled pass C) only for kb > 23.  Three MSD passes, every scatter staged in LDS
 // so that consecutive lanes write consecutive addresses of one destination run:
 //   A  k_hs_count1 / k_hs_binscan / k_hs_binbase / k_hs_scatter1
 //        digits computed from the scalars (zero digits dropped), grouped by bin: per (bin, block
@@ -199,8 +200,8 @@ __global__ __launch_bounds__(SC_TPB) void k_lvl_apply(const uint32_t* __restrict
 // ---------------------------------------------------------------- pass A: digits -> bins
 // a workgroup takes K * HS_TPB scalars (K * HS_TPB * W <= HS_STAGE entries), K per thread
 template <int K>
-__global__ __launch_bounds__(HS_TPB) void k_hs_count1(const uint32_t* __restrict__ scalars, uint32_t n, int c, int nb1,
-                                                      int W, int T, int sh1, uint32_t nbins, uint32_t* __restrict__ hist) {
+__global__ __launch_bounds__(HS_TPB) void k_hs_count1(const uint32_t* __restrict__ scalars, uint32_t n, int c, int W,
+                                                      int T, int sh1, uint32_t nbins, uint32_t* __restrict__ hist) {
   __shared__ uint32_t h[1 << HS_MAX_B1];
   for (uint32_t b = threadIdx.x; b < nbins; b += HS_TPB) h[b] = 0;
   __syncthreads();
@@ -213,7 +214,7 @@ __global__ __launch_bounds__(HS_TPB) void k_hs_count1(const uint32_t* __restrict
     uint32_t carry = 0;
     for (int w = 0; w < W; ++w) {
       uint32_t key, val;
-      if (msmk::digit_entry(s, w, c, nb1, T, n, i, carry, key, val)) atomicAdd(&h[key >> sh1], 1u);
+      if (msmk::digit_entry(s, w, c, T, n, i, carry, key, val)) atomicAdd(&h[key >> sh1], 1u);
     }
   }
   __syncthreads();
@@ -254,7 +255,7 @@ __global__ __launch_bounds__(512) void k_hs_binbase(const uint32_t* __restrict__
 // atomics), then the stage written out linearly: consecutive lanes, consecutive addresses of a run
 template <int K>
 __global__ __launch_bounds__(HS_TPB) void k_hs_scatter1(const uint32_t* __restrict__ scalars, uint32_t n, int c,
-                                                        int nb1, int W, int T, int sh1, uint32_t nbins,
+                                                        int W, int T, int sh1, uint32_t nbins,
                                                         const uint32_t* __restrict__ blkoff,
                                                         const uint32_t* __restrict__ binbase,
                                                         uint2* __restrict__ ent) {
@@ -283,7 +284,7 @@ __global__ __launch_bounds__(HS_TPB) void k_hs_scatter1(const uint32_t* __restri
       e[q][w] = make_uint2(NONE, 0u);
       if (w < W) {
         uint32_t key, val;
-        if (msmk::digit_entry(s, w, c, nb1, T, n, i, carry, key, val) && act) {
+        if (msmk::digit_entry(s, w, c, T, n, i, carry, key, val) && act) {
           e[q][w] = make_uint2(key, val);
           atomicAdd(&cnt[key >> sh1], 1u);
         }

@@ -465,6 +465,31 @@ std::vector<uint8_t> write_mpc(const MpcParams& m) {
   return o;
 }
 
+// The name bytes snarkjs writes: name.substring(0, 64) counts UTF-16 code units, then UTF-8.  A
+// supplementary character (4 UTF-8 bytes) is two units; one cut in half leaves a lone high
+// surrogate, which TextEncoder writes as U+FFFD.  Bytes that are not UTF-8 are copied as one unit.
+static std::string mpc_name_utf8(const std::string& name) {
+  std::string out;
+  size_t units = 0, i = 0;
+  while (i < name.size() && units < 64) {
+    const uint8_t b = (uint8_t)name[i];
+    const size_t len = b < 0x80 ? 1 : (b >> 5) == 6 ? 2 : (b >> 4) == 14 ? 3 : (b >> 3) == 30 ? 4 : 1;
+    if (i + len > name.size()) {
+      out.push_back(name[i++]);
+      ++units;
+      continue;
+    }
+    if (len == 4 && units == 63) {  // only the high surrogate fits
+      out += "\xEF\xBF\xBD";
+      break;
+    }
+    out.append(name, i, len);
+    units += len == 4 ? 2 : 1;
+    i += len;
+  }
+  return out;
+}
+
 void mpc_contribute(MpcParams& m, ChaChaRng& rng, const Affine<HFq>& delta1_before, uint32_t type,
                     const std::string& name, const uint8_t* beacon, size_t beacon_len, uint32_t num_iterations_exp,
                     uint8_t k32[32]) {
@@ -484,15 +509,14 @@ void mpc_contribute(MpcParams& m, ChaChaRng& rng, const Affine<HFq>& delta1_befo
   c.delta_after = g1_times(delta1_before, k);
   c.type = type;
   if (!name.empty()) {
-    const size_t nl = std::min<size_t>(name.size(), 64);
+    const std::string nm = mpc_name_utf8(name);
     c.params.push_back(1);
-    c.params.push_back((uint8_t)nl);
-    c.params.insert(c.params.end(), name.begin(), name.begin() + nl);
+    c.params.push_back((uint8_t)nm.size());
+    c.params.insert(c.params.end(), nm.begin(), nm.end());
   }
   if (type == 1) {
     if (beacon_len > 255 || num_iterations_exp > 255) throw ZkpError(ZKP_ERR_INVALID_ARG, "beacon: parameter too long");
-    c.params.push_back(2);
-    c.params.push_back(1);
+    c.params.push_back(2);  // numIterationsExp: the id, then its one value byte (no length byte)
     c.params.push_back((uint8_t)num_iterations_exp);
     c.params.push_back(3);
     c.params.push_back((uint8_t)beacon_len);

@@ -1,9 +1,6 @@
 // Pippenger MSM engine for BN254 G1/G2 on gfx950.  See msm.hpp for the pipeline.
 #include "msm.hpp"
 
-#include <hipcub/hipcub.hpp>
-#include <rocprim/device/device_radix_sort.hpp>
-
 #include <algorithm>
 #include <cstdlib>
 #include <stdexcept>
@@ -18,8 +15,6 @@ namespace zkp {
 namespace {
 
 constexpr int TPB = 256;
-constexpr int WAVES = TPB / 64;
-constexpr uint32_t MAX_WINDOWS = 128;  // c >= 2
 
 inline unsigned grid_for(size_t n, int tpb = TPB) { return (unsigned)((n + tpb - 1) / tpb); }
 
@@ -34,100 +29,14 @@ __global__ __launch_bounds__(TPB) void k_extend_row(uint32_t* __restrict__ table
   msmk::extend_row<F>(blockIdx.x * TPB + threadIdx.x, table, n, dbl, t);
 }
 
-// pass 1 of the compacted digit emission: nonzero digits per (window, block)
-__global__ __launch_bounds__(TPB) void k_digit_count(const uint32_t* __restrict__ scalars, uint32_t n, int c, int nb1,
-                                                     int W, uint32_t* __restrict__ bcnt) {
-  __shared__ uint32_t cnt[MAX_WINDOWS];
-  for (uint32_t w = threadIdx.x; w < (uint32_t)W; w += TPB) cnt[w] = 0;
-  __syncthreads();
-  const uint32_t i = blockIdx.x * TPB + threadIdx.x;
-  const bool active = i < n;
-  uint32_t s[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-  if (active) msmk::load_scalar(scalars, i, s);
-  uint32_t carry = 0;
-  bool neg;
-  for (int w = 0; w < W; ++w) {
-    const uint32_t mag = msmk::digit_mag(s, w, c, nb1, carry, neg);
-    const uint64_t m = __ballot(active && mag != 0);
-    if ((threadIdx.x & 63) == 0) atomicAdd(&cnt[w], (uint32_t)__popcll(m));
-  }
-  __syncthreads();
-  for (uint32_t w = threadIdx.x; w < (uint32_t)W; w += TPB) bcnt[(size_t)w * gridDim.x + blockIdx.x] = cnt[w];
-}
-
-// pass 2: write (key, base | sign) of every nonzero digit at
-//   boff[window][block] + (entries of earlier waves of the block) + (earlier lanes of the wave)
-// -> window-major, point order within a window (deterministic)
-__global__ __launch_bounds__(TPB) void k_digit_write(const uint32_t* __restrict__ scalars, uint32_t n, int c, int nb1,
-                                                     int W, int T, const uint32_t* __restrict__ boff,
-                                                     uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
-  __shared__ uint32_t wcnt[MAX_WINDOWS][WAVES];
-  const uint32_t i = blockIdx.x * TPB + threadIdx.x;
-  const int wave = threadIdx.x >> 6;
-  const bool active = i < n;
-  uint32_t s[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-  if (active) msmk::load_scalar(scalars, i, s);
-  uint32_t carry = 0;
-  bool neg;
-  for (int w = 0; w < W; ++w) {
-    const uint32_t mag = msmk::digit_mag(s, w, c, nb1, carry, neg);
-    const uint64_t m = __ballot(active && mag != 0);
-    if ((threadIdx.x & 63) == 0) wcnt[w][wave] = (uint32_t)__popcll(m);
-  }
-  __syncthreads();
-  carry = 0;
-  for (int w = 0; w < W; ++w) {
-    uint32_t key, val;
-    const bool valid = msmk::digit_entry(s, w, c, nb1, T, n, i, carry, key, val) && active;
-    const uint64_t m = __ballot(valid);
-    if (valid) {
-      uint32_t base = boff[(size_t)w * gridDim.x + blockIdx.x];
-      for (int v = 0; v < wave; ++v) base += wcnt[w][v];
-      const uint32_t pos = base + lane_rank(m);
-      keys[pos] = key;
-      vals[pos] = val;
-    }
-  }
-}
-
-// dense emission (uniform scalars: nearly every digit is nonzero): entry w*n + i for every
-// (window, point), a zero digit keyed `sentinel` (= the bucket count, sorted past every
-// bucket) -- no counting pass, no scan, no host round trip for the entry count
-__global__ __launch_bounds__(TPB) void k_digit_write_dense(const uint32_t* __restrict__ scalars, uint32_t n, int c,
-                                                           int nb1, int W, int T, uint32_t sentinel,
-                                                           uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
-  const uint32_t i = blockIdx.x * TPB + threadIdx.x;
-  if (i >= n) return;
-  uint32_t s[9];
-  msmk::load_scalar(scalars, i, s);
-  uint32_t carry = 0;
-  for (int w = 0; w < W; ++w) {
-    uint32_t key, val;
-    const bool valid = msmk::digit_entry(s, w, c, nb1, T, n, i, carry, key, val);
-    keys[(size_t)w * n + i] = valid ? key : sentinel;
-    vals[(size_t)w * n + i] = val;
-  }
-}
-
-__global__ __launch_bounds__(TPB) void k_bounds(const uint32_t* __restrict__ keys, uint32_t total,
-                                                uint32_t* __restrict__ start, uint32_t* __restrict__ end) {
-  msmk::bounds(blockIdx.x * TPB + threadIdx.x, keys, total, start, end);
-}
-__global__ __launch_bounds__(TPB) void k_task_counts(const uint32_t* __restrict__ start,
-                                                     const uint32_t* __restrict__ end, uint32_t nb, uint32_t S,
-                                                     uint32_t* __restrict__ cnt) {
-  msmk::task_counts(blockIdx.x * TPB + threadIdx.x, start, end, nb, S, cnt);
-}
 // G2 (Fq2) accumulation and bucket merges (the wide finish kernels): without a bound the
 // compiler takes 256 VGPRs + AGPRs (one wave per SIMD, nothing to hide the mad-chain
 // latency); two waves per SIMD (a few spilled dwords; accumulation measured 5.24 -> 4.55 ms
 // per 6.4 M-point G2 MSM)
-#ifndef ZKP_G1_ACC_WAVES
-#define ZKP_G1_ACC_WAVES 1  // 1 = no bound (118 VGPRs, 4 waves); a prefetching gather at 3 or 4 waves measured slower
-#endif
+// (G1: no bound, 118 VGPRs and four waves per SIMD; 3 / 5 / 6 waves measured slower, profiles/acc_waves_r03.txt)
 template <class F>
 struct AccWaves {
-  static constexpr int value = FWords<F>::W == 16 ? 2 : ZKP_G1_ACC_WAVES;
+  static constexpr int value = FWords<F>::W == 16 ? 2 : 1;
 };
 template <class F>
 struct MergeWaves {
@@ -193,12 +102,6 @@ __global__ __launch_bounds__(TPB) void k_subset_first(const uint32_t* __restrict
                                                       uint32_t fan, uint32_t* __restrict__ out) {
   msmk::subset_first<F>(blockIdx.x * TPB + threadIdx.x, s_in, t_in, G, lgP, fan, out);
 }
-template <class F>
-__global__ __launch_bounds__(TPB) void k_subset_level(const uint32_t* __restrict__ in, uint32_t nseg, uint32_t n_in,
-                                                      uint32_t fan, uint32_t* __restrict__ out) {
-  msmk::subset_level<F>(blockIdx.x * TPB + threadIdx.x, in, nseg, n_in, fan, out);
-}
-
 // (no waves-per-SIMD bound: a latency-bound tree, one wave per SIMD suffices; bounding the G2 variant
 // to two waves spills ~290 dwords)
 template <class F>
@@ -214,54 +117,9 @@ __global__ __launch_bounds__(msmk::TREE_TPB) void k_subset_tree_next(
   __shared__ uint32_t lds[msmk::XyzzLimbs<F>::N * (msmk::TREE_TPB / 2)];
   msmk::subset_tree_next<F>(in, n_in, n_out, blockIdx.y, blockIdx.x, lds, out);
 }
-// largest first-level tree grid (workgroups); larger subset sums (the proof's MSMs) start with
-// full-lane fan-in chains (ZKP_TREE_FIRST_MAX overrides)
-// (read per finish, so tests can switch them per prover)
-static size_t tree_first_max() {
-  const char* e = std::getenv("ZKP_TREE_FIRST_MAX");
-  return e ? (size_t)std::atol(e) : (size_t)512;
-}
-static bool subset_tree() {
-  const char* e = std::getenv("ZKP_SUBSET_TREE");
-  return !(e && std::atoi(e) == 0);
-}
-
-// Bucket-key sort: rocprim onesweep with 9-bit digits (512-way, 2 passes for the 17/18-bit keys
-// of c = 18/19) instead of the default 8-bit (3 passes): measured 35.7 vs 36.1 ms per proof;
-// other key widths keep the default (e.g. 15 bits: 2 passes either way, default faster).
-// ZKP_SORT_BITS=8 forces the default.  (A 10-bit config for the H plan's 19-bit keys, 2
-// passes instead of 3, measured slower: 1.6 + 1.45 ms against 3 x 0.73 ms.)
-using SortCfg9 = rocprim::radix_sort_config<
-    rocprim::default_config, rocprim::default_config,
-    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<256, 12>, rocprim::kernel_config<512, 12>, 9,
-                                        rocprim::block_radix_rank_algorithm::match>>;
-static int sort_bits() {
-  static int v = [] {
-    const char* e = std::getenv("ZKP_SORT_BITS");
-    return e ? std::atoi(e) : 9;
-  }();
-  return v;
-}
-hipError_t sort_pairs(void* tmp, size_t& tmp_bytes, const uint32_t* kin, uint32_t* kout, const uint32_t* vin,
-                      uint32_t* vout, size_t n, int end_bit, hipStream_t st) {
-  if (sort_bits() == 9 && (end_bit == 17 || end_bit == 18))  // 2 passes of 9 instead of 3 of 8
-    return rocprim::radix_sort_pairs<SortCfg9>(tmp, tmp_bytes, kin, kout, vin, vout, n, 0u, (unsigned)end_bit, st);
-  return rocprim::radix_sort_pairs(tmp, tmp_bytes, kin, kout, vin, vout, n, 0u, (unsigned)end_bit, st);
-}
-
-// ---- bucket binning (opt-in, ZKP_PLAN_SORT=bins): grouping the nonzero digits by bucket as a
-// two-level counting sort with no decoupled look-back (every workgroup independent, so it
-// keeps its speed beside the long accumulation kernels of other streams, unlike a onesweep
-// radix sort):
-//   k_bin_hist     per (coarse bin = top <= 9 key bits, digit block) counts in LDS
-//   scan           -> every block's write offset inside every coarse bin (bin-major)
-//   k_bin_scatter  recomputes the digits, writes (fine key bits, base|sign) into the bins
-//   k_chunk_*      each bin grouped by its fine key bits (below), bucket bounds on the way
-// Entry order inside a bucket is not fixed (LDS atomics): the bucket sum is the same group
-// element in any order, so the MSM result is unchanged.
-constexpr int BIN_R = 16;          // scalars per thread in the binning passes (long runs per bin)
-constexpr int MAX_COARSE_BITS = 9;
-constexpr int MAX_FINE_BITS = 13;  // 32 KiB LDS histogram
+// largest first-level tree grid (workgroups): larger subset sums (the proof's H MSM: 18 sums of 2^16
+// values) start with a full-lane fan-in chain level (profiles/subset_tree_r02.txt)
+constexpr size_t TREE_FIRST_MAX = 512;
 
 // count (or, with rank != nullptr, claim a slot for) one entry in LDS counter h[b]; lanes of a
 // wave that all hit the same counter (the skewed buckets of 0/1 witness values) use one atomic
@@ -278,135 +136,6 @@ __device__ __forceinline__ uint32_t lds_claim(uint32_t* h, uint32_t b, bool vali
     return base + lane_rank(m);
   }
   return valid ? atomicAdd(&h[b], 1u) : 0u;
-}
-
-__global__ __launch_bounds__(TPB) void k_bin_hist(const uint32_t* __restrict__ scalars, uint32_t n, int c, int nb1,
-                                                  int W, int T, int fb, uint32_t nbins, uint32_t* __restrict__ hist) {
-  __shared__ uint32_t h[1 << MAX_COARSE_BITS];
-  for (uint32_t b = threadIdx.x; b < nbins; b += TPB) h[b] = 0;
-  __syncthreads();
-  for (int r = 0; r < BIN_R; ++r) {
-    const uint32_t i = (blockIdx.x * BIN_R + r) * TPB + threadIdx.x;
-    const bool active = i < n;
-    uint32_t s[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-    if (active) msmk::load_scalar(scalars, i, s);
-    uint32_t carry = 0;
-    for (int w = 0; w < W; ++w) {
-      uint32_t key, val;
-      const bool valid = msmk::digit_entry(s, w, c, nb1, T, n, i, carry, key, val) && active;
-      lds_claim(h, key >> fb, valid);
-    }
-  }
-  __syncthreads();
-  for (uint32_t b = threadIdx.x; b < nbins; b += TPB) hist[(size_t)b * gridDim.x + blockIdx.x] = h[b];
-}
-
-__global__ __launch_bounds__(TPB) void k_bin_scatter(const uint32_t* __restrict__ scalars, uint32_t n, int c, int nb1,
-                                                     int W, int T, int fb, uint32_t nbins, const uint32_t* __restrict__ hoff,
-                                                     uint32_t* __restrict__ fine, uint32_t* __restrict__ vals) {
-  __shared__ uint32_t cur[1 << MAX_COARSE_BITS];
-  for (uint32_t b = threadIdx.x; b < nbins; b += TPB) cur[b] = hoff[(size_t)b * gridDim.x + blockIdx.x];
-  __syncthreads();
-  const uint32_t fmask = (1u << fb) - 1;
-  for (int r = 0; r < BIN_R; ++r) {
-    const uint32_t i = (blockIdx.x * BIN_R + r) * TPB + threadIdx.x;
-    const bool active = i < n;
-    uint32_t s[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-    if (active) msmk::load_scalar(scalars, i, s);
-    uint32_t carry = 0;
-    for (int w = 0; w < W; ++w) {
-      uint32_t key, val;
-      const bool valid = msmk::digit_entry(s, w, c, nb1, T, n, i, carry, key, val) && active;
-      const uint32_t pos = lds_claim(cur, key >> fb, valid);
-      if (valid) {
-        fine[pos] = key & fmask;
-        vals[pos] = val;
-      }
-    }
-  }
-}
-
-// pass 2 works on chunks of <= BIN_CHUNK entries of one coarse bin (a skewed bin -- the
-// bucket of every witness value 1 -- spreads over many workgroups):
-//   k_chunk_count  chunks per bin;  scan -> choff
-//   k_chunk_hist   per chunk LDS histogram of the fine bits -> hist2[nf*choff[b] + f*nch_b + c]
-//   scan           -> global sorted position of every (bin, fine, chunk) run
-//   k_chunk_scatter / k_chunk_bounds  the entries, and every bucket's [start, end)
-constexpr uint32_t BIN_CHUNK = 16384;
-
-__global__ __launch_bounds__(TPB) void k_chunk_count(const uint32_t* __restrict__ hoff, uint32_t nblk, uint32_t nbins,
-                                                     uint32_t* __restrict__ nch) {
-  const uint32_t b = blockIdx.x * TPB + threadIdx.x;
-  if (b > nbins) return;
-  nch[b] = b == nbins ? 0u
-                      : (hoff[(size_t)(b + 1) * nblk] - hoff[(size_t)b * nblk] + BIN_CHUNK - 1) / BIN_CHUNK;
-}
-
-struct ChunkRange {
-  uint32_t b, c, nch, lo, hi;
-};
-__device__ __forceinline__ bool chunk_range(const uint32_t* __restrict__ hoff, uint32_t nblk,
-                                            const uint32_t* __restrict__ choff, uint32_t nbins, uint32_t id,
-                                            ChunkRange& r) {
-  if (id >= choff[nbins]) return false;
-  r.b = msmk::seg_search(choff, nbins, id);
-  r.c = id - choff[r.b];
-  r.nch = choff[r.b + 1] - choff[r.b];
-  const uint32_t blo = hoff[(size_t)r.b * nblk], bhi = hoff[(size_t)(r.b + 1) * nblk];
-  r.lo = blo + r.c * BIN_CHUNK;
-  r.hi = msmk::umin(bhi, r.lo + BIN_CHUNK);
-  return true;
-}
-
-__global__ __launch_bounds__(TPB) void k_chunk_hist(const uint32_t* __restrict__ fine, const uint32_t* __restrict__ hoff,
-                                                    uint32_t nblk, const uint32_t* __restrict__ choff, uint32_t nbins,
-                                                    int fb, uint32_t* __restrict__ hist2) {
-  __shared__ uint32_t h[1 << MAX_FINE_BITS];
-  ChunkRange r;
-  if (!chunk_range(hoff, nblk, choff, nbins, blockIdx.x, r)) return;
-  const uint32_t nf = 1u << fb;
-  for (uint32_t f = threadIdx.x; f < nf; f += TPB) h[f] = 0;
-  __syncthreads();
-  for (uint32_t j0 = r.lo; j0 < r.hi; j0 += TPB) {
-    const uint32_t j = j0 + threadIdx.x;
-    lds_claim(h, j < r.hi ? fine[j] : 0u, j < r.hi);
-  }
-  __syncthreads();
-  const size_t base = (size_t)nf * choff[r.b] + r.c;
-  for (uint32_t f = threadIdx.x; f < nf; f += TPB) hist2[base + (size_t)f * r.nch] = h[f];
-}
-
-__global__ __launch_bounds__(TPB) void k_chunk_scatter(const uint32_t* __restrict__ fine,
-                                                       const uint32_t* __restrict__ vin,
-                                                       const uint32_t* __restrict__ hoff, uint32_t nblk,
-                                                       const uint32_t* __restrict__ choff, uint32_t nbins, int fb,
-                                                       const uint32_t* __restrict__ hoff2,
-                                                       uint32_t* __restrict__ vout) {
-  __shared__ uint32_t cur[1 << MAX_FINE_BITS];
-  ChunkRange r;
-  if (!chunk_range(hoff, nblk, choff, nbins, blockIdx.x, r)) return;
-  const uint32_t nf = 1u << fb;
-  const size_t base = (size_t)nf * choff[r.b] + r.c;
-  for (uint32_t f = threadIdx.x; f < nf; f += TPB) cur[f] = hoff2[base + (size_t)f * r.nch];
-  __syncthreads();
-  for (uint32_t j0 = r.lo; j0 < r.hi; j0 += TPB) {
-    const uint32_t j = j0 + threadIdx.x;
-    const bool ok = j < r.hi;
-    const uint32_t pos = lds_claim(cur, ok ? fine[j] : 0u, ok);
-    if (ok) vout[pos] = vin[j];
-  }
-}
-
-__global__ __launch_bounds__(TPB) void k_chunk_bounds(const uint32_t* __restrict__ choff, int fb, uint32_t nb,
-                                                      const uint32_t* __restrict__ hoff2, uint32_t* __restrict__ start,
-                                                      uint32_t* __restrict__ end) {
-  const uint32_t k = blockIdx.x * TPB + threadIdx.x;
-  if (k >= nb) return;
-  const uint32_t nf = 1u << fb, b = k >> fb, f = k & (nf - 1);
-  const uint32_t nch = choff[b + 1] - choff[b];
-  const size_t base = (size_t)nf * choff[b];
-  start[k] = hoff2[base + (size_t)f * nch];
-  end[k] = hoff2[base + (size_t)(f + 1) * nch];
 }
 
 #include "hsort_kernels.hpp"
@@ -447,41 +176,27 @@ void run_finish(const MsmPlan& plan, uint32_t* part_a, uint32_t* part_b, uint32_
   hipLaunchKernelGGL(k_merge_final<F>, dim3(grid_for(nb)), dim3(TPB), 0, st, part_a, part_b, plan.task_off(), nb,
                      (uint32_t)prm.S2, plan.merge_levels(), buckets);
   // bucket reduction: segments, then the K = lgP + 1 subset sums per group by L-ary tree
-  const uint32_t M = (uint32_t)prm.M, lgP = (uint32_t)prm.lgP(), K = (uint32_t)prm.K(), fan = (uint32_t)prm.L;
+  const uint32_t M = (uint32_t)prm.M, lgP = (uint32_t)prm.lgP(), K = (uint32_t)prm.K();
   hipLaunchKernelGGL(k_reduce_segments<F>, dim3(grid_for((size_t)G * (half / M))), dim3(TPB), 0, st, buckets, G, half,
                      M, seg_s, seg_t);
+  // workgroup LDS trees: 2 * TREE_TPB values per workgroup and launch level
   int cur = 0;
-  if (subset_tree()) {  // workgroup LDS trees: 2 * TREE_TPB values per workgroup and launch level
-    constexpr uint32_t CH = 2 * msmk::TREE_TPB;
-    uint32_t n = ((1u << lgP) + CH - 1) / CH;
-    if ((size_t)G * K * n <= tree_first_max()) {  // about one round of workgroups: the tree from the inputs
-      hipLaunchKernelGGL(k_subset_tree_first<F>, dim3(n, G * K), dim3(msmk::TREE_TPB), 0, st, seg_s, seg_t, lgP, n,
-                         sub[0]);
-    } else {  // many inputs (the H MSM: K x 2^16): full-lane fan-in chains first (short: the trees
-              // above them take the rest), then trees
-      const uint32_t cf = std::min<uint32_t>(fan, msmk::TREE_CHAIN_FAN);
-      n = (((1u << lgP) + 2 * cf - 1) / (2 * cf));
-      hipLaunchKernelGGL(k_subset_first<F>, dim3(grid_for((size_t)G * K * n)), dim3(TPB), 0, st, seg_s, seg_t, G,
-                         lgP, cf, sub[0]);
-    }
-    while (n > 1) {
-      const uint32_t next = (n + CH - 1) / CH;
-      hipLaunchKernelGGL(k_subset_tree_next<F>, dim3(next, G * K), dim3(msmk::TREE_TPB), 0, st, sub[cur], n, next,
-                         sub[cur ^ 1]);
-      cur ^= 1;
-      n = next;
-    }
-    HIPX(hipGetLastError());
-    HIPX(hipMemcpyAsync(d_out, sub[cur], (size_t)G * K * xyzz_bytes, hipMemcpyDeviceToDevice, st));
-    return;
+  constexpr uint32_t CH = 2 * msmk::TREE_TPB;
+  uint32_t n = ((1u << lgP) + CH - 1) / CH;
+  if ((size_t)G * K * n <= TREE_FIRST_MAX) {  // about one round of workgroups: the tree from the inputs
+    hipLaunchKernelGGL(k_subset_tree_first<F>, dim3(n, G * K), dim3(msmk::TREE_TPB), 0, st, seg_s, seg_t, lgP, n,
+                       sub[0]);
+  } else {  // many inputs (the H MSM: K x 2^16): a full-lane fan-in chain level first (short: the
+            // trees above it take the rest), then trees
+    const uint32_t cf = msmk::TREE_CHAIN_FAN;
+    n = (((1u << lgP) + 2 * cf - 1) / (2 * cf));
+    hipLaunchKernelGGL(k_subset_first<F>, dim3(grid_for((size_t)G * K * n)), dim3(TPB), 0, st, seg_s, seg_t, G, lgP,
+                       cf, sub[0]);
   }
-  uint32_t n = (((1u << lgP) + 2 * fan - 1) / (2 * fan));
-  hipLaunchKernelGGL(k_subset_first<F>, dim3(grid_for((size_t)G * K * n)), dim3(TPB), 0, st, seg_s, seg_t, G, lgP,
-                     fan, sub[0]);
   while (n > 1) {
-    const uint32_t next = (n + fan - 1) / fan;
-    hipLaunchKernelGGL(k_subset_level<F>, dim3(grid_for((size_t)G * K * next)), dim3(TPB), 0, st, sub[cur], G * K,
-                       n, fan, sub[cur ^ 1]);
+    const uint32_t next = (n + CH - 1) / CH;
+    hipLaunchKernelGGL(k_subset_tree_next<F>, dim3(next, G * K), dim3(msmk::TREE_TPB), 0, st, sub[cur], n, next,
+                       sub[cur ^ 1]);
     cur ^= 1;
     n = next;
   }
@@ -493,8 +208,7 @@ void run_finish(const MsmPlan& plan, uint32_t* part_a, uint32_t* part_b, uint32_
 
 // ------------------------------------------------------------------ MsmBases
 
-MsmBases::MsmBases(Curve curve, size_t n, int c, int depth, int nb1)
-    : curve_(curve), n_(n), c_(c), depth_(depth), nb1_(nb1) {
+MsmBases::MsmBases(Curve curve, size_t n, int c, int depth) : curve_(curve), n_(n), c_(c), depth_(depth) {
   if (depth < 1 || c < 2) throw std::runtime_error("MsmBases: bad parameters");
   if ((size_t)depth * std::max<size_t>(n, 1) >= (size_t(1) << 31))
     throw std::runtime_error("MsmBases: depth * n must stay below 2^31 (31-bit base indices)");
@@ -509,11 +223,10 @@ MsmBases::~MsmBases() {
 void MsmBases::extend(hipStream_t st) {
   if (n_ == 0) return;
   for (int t = 1; t < depth_; ++t) {
-    const int dbl = t - 1 < nb1_ ? c_ : c_ - 1;  // the width of window t - 1
     if (curve_ == Curve::G1)
-      hipLaunchKernelGGL(k_extend_row<Fq>, dim3(grid_for(n_)), dim3(TPB), 0, st, d_, (uint32_t)n_, dbl, t);
+      hipLaunchKernelGGL(k_extend_row<Fq>, dim3(grid_for(n_)), dim3(TPB), 0, st, d_, (uint32_t)n_, c_, t);
     else
-      hipLaunchKernelGGL(k_extend_row<Fq2>, dim3(grid_for(n_)), dim3(TPB), 0, st, d_, (uint32_t)n_, dbl, t);
+      hipLaunchKernelGGL(k_extend_row<Fq2>, dim3(grid_for(n_)), dim3(TPB), 0, st, d_, (uint32_t)n_, c_, t);
   }
   HIPX(hipGetLastError());
 }
@@ -522,136 +235,74 @@ void MsmBases::extend(hipStream_t st) {
 
 MsmPlan::MsmPlan(size_t max_n, const MsmParams& prm, hipStream_t stream)
     : prm_(prm), max_n_(std::max<size_t>(max_n, 1)), stream_(stream) {
-  if (prm_.windows > (int)MAX_WINDOWS) throw std::runtime_error("MSM: too many windows");
+  if (prm_.c < MsmParams::MIN_C || prm_.c > MsmParams::MAX_C || prm_.windows > HS_STAGE / HS_TPB)
+    throw std::invalid_argument("MSM: window bits outside the plan's range");
   if (max_n_ * prm_.depth >= (size_t(1) << 31)) throw std::runtime_error("MSM size too large for 31-bit base indices");
   nbuckets_ = prm_.buckets();
   max_entries_ = max_n_ * prm_.windows;
   if (max_entries_ >= 0xffffffffull) throw std::runtime_error("MSM size too large for 32-bit entry indices");
   max_tasks_ = (max_entries_ + prm_.S - 1) / prm_.S + nbuckets_;
   merge_levels_ = msm_merge_levels(max_n_, prm_);
-  HIPX(hipMalloc(&keys_, max_entries_ * 4));
-  HIPX(hipMalloc(&vals_, max_entries_ * 4));
-  HIPX(hipMalloc(&keys_sorted_, max_entries_ * 4));
   HIPX(hipMalloc(&vals_sorted_, max_entries_ * 4));
   HIPX(hipMalloc(&bstart_, (nbuckets_ + 1) * 4));
   HIPX(hipMalloc(&bend_, (nbuckets_ + 1) * 4));
   HIPX(hipMalloc(&cnt_, (nbuckets_ + 1) * 4));
   HIPX(hipMalloc(&off_task_, (nbuckets_ + 1) * 4));
-  {
-    const char* e = std::getenv("ZKP_TASK_ORDER");
-    use_perm_ = !(e && std::string(e) == "bucket");
-    if (use_perm_) {
-      HIPX(hipMalloc(&perm_, max_tasks_ * 4));
-      const size_t nh = (size_t)(prm_.S + 1) * grid_for(max_tasks_);
-      HIPX(hipMalloc(&tl_hist_, nh * 4));
-      HIPX(hipMalloc(&tl_off_, nh * 4));
-    }
-  }
+  HIPX(hipMalloc(&perm_, max_tasks_ * 4));
+  const size_t ntl = (size_t)(prm_.S + 1) * grid_for(max_tasks_);
+  HIPX(hipMalloc(&tl_hist_, ntl * 4));
+  HIPX(hipMalloc(&tl_off_, ntl * 4));
   off_lvl_.assign(merge_levels_, nullptr);
   if (merge_levels_ > 0) {
     HIPX(hipMalloc(&lvl_all_, (size_t)merge_levels_ * (nbuckets_ + 1) * 4));
     for (int l = 0; l < merge_levels_; ++l) off_lvl_[l] = lvl_all_ + (size_t)l * (nbuckets_ + 1);
     HIPX(hipMalloc(&lvl_tsum_, (size_t)merge_levels_ * scan_tiles_for(nbuckets_ + 1) * 4));
   }
-  const size_t ncnt = (size_t)prm_.windows * grid_for(max_n_) + 1;  // per (window, digit block) counts
-  HIPX(hipMalloc(&bcnt_, ncnt * 4));
-  HIPX(hipMalloc(&boff_, ncnt * 4));
-  HIPX(hipHostMalloc(&h_valid_, 4, hipHostMallocDefault));
-  {
-    int kb = 0;
-    while ((size_t(1) << kb) < nbuckets_) ++kb;
-    const int coarse = std::min(kb, MAX_COARSE_BITS);
-    fine_bits_ = kb - coarse;
-    nbins_ = (uint32_t)((nbuckets_ + (size_t(1) << fine_bits_) - 1) >> fine_bits_);
-    // opt-in (ZKP_PLAN_SORT=bins): correct, contention-robust, but its register-to-global
-    // scatters are not staged through LDS and measured slower than the radix sort (serial
-    // 5.2 vs 4.0 ms of plan kernels per proof; proof 32.8 vs 31.0 ms)
-    const char* e = std::getenv("ZKP_PLAN_SORT");
-    use_bins_ = fine_bits_ <= MAX_FINE_BITS && e && std::string(e) == "bins";
-    if (use_bins_) {
-      const size_t nh = (size_t)nbins_ * grid_for(max_n_, TPB * BIN_R) + 1;
-      HIPX(hipMalloc(&hist_, nh * 4));
-      HIPX(hipMalloc(&hoff_, nh * 4));
-      max_chunks_ = nbins_ + (max_entries_ + BIN_CHUNK - 1) / BIN_CHUNK;
-      const size_t nh2 = (max_chunks_ << fine_bits_) + 1;
-      HIPX(hipMalloc(&nch_, (nbins_ + 1) * 4));
-      HIPX(hipMalloc(&choff_, (nbins_ + 1) * 4));
-      HIPX(hipMalloc(&hist2_, nh2 * 4));
-      HIPX(hipMalloc(&hoff2_, nh2 * 4));
-    }
-  }
-  {
-    int kb = 1;
-    while ((size_t(1) << kb) < nbuckets_) ++kb;
-    hs_b3_ = std::min(kb, HS_B3);
-    hs_b2_ = (kb - hs_b3_) / 2;
-    const int b1 = kb - hs_b3_ - hs_b2_;
-    hs_nbins_ = (uint32_t)((nbuckets_ + (size_t(1) << (hs_b2_ + hs_b3_)) - 1) >> (hs_b2_ + hs_b3_));
-    hs_k_ = std::max(1, std::min(4, HS_STAGE / (HS_TPB * prm_.windows)));
-    if (hs_k_ == 3) hs_k_ = 2;
-    hs_nblk_ = (uint32_t)((max_n_ + hs_k_ * HS_TPB - 1) / (hs_k_ * HS_TPB));
-    hs_max_tiles_ = (uint32_t)((max_entries_ + HS_TILE - 1) / HS_TILE + hs_nbins_);
-    const char* e = std::getenv("ZKP_H_SORT");
-    use_hsort_ = prm_.windows <= HS_STAGE / HS_TPB && b1 <= HS_MAX_B1 && hs_b2_ <= HS_MAX_B2 &&
-                 !(e && std::string(e) == "rocprim");
-    const char* ew = std::getenv("ZKP_W_SORT");
-    use_wsort_ = use_hsort_ && !(ew && std::string(ew) == "rocprim");
-    const char* et = std::getenv("ZKP_HS_TILED_C");
-    hs_tiled_c_ = et && std::atoi(et) == 1;
-    const uint32_t nq = hs_nbins_ << hs_b2_;
-    hs_max_tiles3_ = (uint32_t)((max_entries_ + HS_TILE - 1) / HS_TILE + nq);
-    size_t scan_n = nbuckets_ + 1;
-    if (use_hsort_) {
-      const size_t nh3 = ((size_t)hs_max_tiles3_ << hs_b3_) + 1;
-      HIPX(hipMalloc(&hs_toff3_, ((size_t)nq + 1) * 4));
-      HIPX(hipMalloc(&hs_hist3_, nh3 * 4));
-      HIPX(hipMalloc(&hs_off3_, nh3 * 4));
-      scan_n = std::max(scan_n, nh3);
-      const size_t nh = (size_t)hs_nbins_ * hs_nblk_, nh2 = (size_t)hs_max_tiles_ << hs_b2_;
-      HIPX(hipMalloc(&hs_hist_, nh * 4));
-      HIPX(hipMalloc(&hs_blkoff_, nh * 4));
-      HIPX(hipMalloc(&hs_bintot_, (hs_nbins_ + 1) * 4));
-      HIPX(hipMalloc(&hs_binbase_, (hs_nbins_ + 1) * 4));
-      HIPX(hipMalloc(&hs_toff_, (hs_nbins_ + 1) * 4));
-      HIPX(hipMalloc(&hs_hist2_, nh2 * 4));
-      HIPX(hipMalloc(&hs_off2_, nh2 * 4));
-      HIPX(hipMalloc(&hs_subbase_, (((size_t)hs_nbins_ << hs_b2_) + 1) * 4));
-      HIPX(hipMalloc(&hs_ent_a_, max_entries_ * 8));
-      HIPX(hipMalloc(&hs_ent_b_, max_entries_ * 8));
-      scan_n = std::max(scan_n, nh2);
-    }
-    if (use_perm_) scan_n = std::max(scan_n, (size_t)(prm_.S + 1) * grid_for(max_tasks_));
-    tsum_len_ = scan_tiles_for(scan_n) + 1;
-    HIPX(hipMalloc(&tsum_, tsum_len_ * 4));
-  }
-  HIPX(sort_pairs(nullptr, sort_tmp_bytes_, keys_, keys_sorted_, vals_, vals_sorted_, max_entries_, prm_.c - 1,
-                  stream_));
-  while ((size_t(1) << dense_bits_) <= nbuckets_) ++dense_bits_;
-  {
-    size_t dense_tmp = 0;
-    HIPX(sort_pairs(nullptr, dense_tmp, keys_, keys_sorted_, vals_, vals_sorted_, max_entries_, dense_bits_, stream_));
-    sort_tmp_bytes_ = std::max(sort_tmp_bytes_, dense_tmp);
-  }
-  HIPX(hipMalloc(&sort_tmp_, std::max<size_t>(sort_tmp_bytes_, 4)));
-  const size_t nscan = std::max(std::max(std::max(nbuckets_ + 1, ncnt), (size_t)nbins_ * grid_for(max_n_, TPB * BIN_R) + 1),
-                                (max_chunks_ << fine_bits_) + 1);
-  HIPX(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_tmp_bytes_, cnt_, off_task_, (int)nscan, stream_));
-  HIPX(hipMalloc(&scan_tmp_, std::max<size_t>(scan_tmp_bytes_, 4)));
+  // bucket-key bits kb = b1 (bin) + b2 (sub-bin) + b3 (bucket in sub-bin): b3 = 5 for the one-
+  // workgroup-per-sub-bin pass C (k_hs_fine), up to 9 (tiled pass C) when kb > 23 (c > 20 with
+  // several bucket groups); b1, b2 <= 9
+  int kb = 1;
+  while ((size_t(1) << kb) < nbuckets_) ++kb;
+  hs_b3_ = std::max(std::min(kb, HS_B3), kb - HS_MAX_B1 - HS_MAX_B2);
+  hs_b2_ = (kb - hs_b3_) / 2;
+  const int b1 = kb - hs_b3_ - hs_b2_;
+  if (b1 > HS_MAX_B1 || hs_b2_ > HS_MAX_B2 || hs_b3_ > HS_MAX_B2)
+    throw std::invalid_argument("MSM: too many buckets for the bucket sort (window bits x bucket groups)");
+  hs_nbins_ = (uint32_t)((nbuckets_ + (size_t(1) << (hs_b2_ + hs_b3_)) - 1) >> (hs_b2_ + hs_b3_));
+  hs_k_ = std::max(1, std::min(4, HS_STAGE / (HS_TPB * prm_.windows)));
+  if (hs_k_ == 3) hs_k_ = 2;
+  hs_nblk_ = (uint32_t)((max_n_ + hs_k_ * HS_TPB - 1) / (hs_k_ * HS_TPB));
+  hs_max_tiles_ = (uint32_t)((max_entries_ + HS_TILE - 1) / HS_TILE + hs_nbins_);
+  const uint32_t nq = hs_nbins_ << hs_b2_;
+  hs_max_tiles3_ = (uint32_t)((max_entries_ + HS_TILE - 1) / HS_TILE + nq);
+  const size_t nh3 = ((size_t)hs_max_tiles3_ << hs_b3_) + 1;
+  HIPX(hipMalloc(&hs_toff3_, ((size_t)nq + 1) * 4));
+  HIPX(hipMalloc(&hs_hist3_, nh3 * 4));
+  HIPX(hipMalloc(&hs_off3_, nh3 * 4));
+  const size_t nh = (size_t)hs_nbins_ * hs_nblk_, nh2 = (size_t)hs_max_tiles_ << hs_b2_;
+  HIPX(hipMalloc(&hs_hist_, nh * 4));
+  HIPX(hipMalloc(&hs_blkoff_, nh * 4));
+  HIPX(hipMalloc(&hs_bintot_, (hs_nbins_ + 1) * 4));
+  HIPX(hipMalloc(&hs_binbase_, (hs_nbins_ + 1) * 4));
+  HIPX(hipMalloc(&hs_toff_, (hs_nbins_ + 1) * 4));
+  HIPX(hipMalloc(&hs_hist2_, nh2 * 4));
+  HIPX(hipMalloc(&hs_off2_, nh2 * 4));
+  HIPX(hipMalloc(&hs_subbase_, ((size_t)nq + 1) * 4));
+  HIPX(hipMalloc(&hs_ent_a_, max_entries_ * 8));
+  HIPX(hipMalloc(&hs_ent_b_, max_entries_ * 8));
+  const size_t scan_n = std::max(std::max(nbuckets_ + 1, nh3), std::max(nh2, ntl));
+  HIPX(hipMalloc(&tsum_, (scan_tiles_for(scan_n) + 1) * 4));
   HIPX(hipEventCreateWithFlags(&ready_, hipEventDisableTiming));
 }
 
 MsmPlan::~MsmPlan() {
   if (ready_) (void)hipEventDestroy(ready_);
-  if (h_valid_) (void)hipHostFree(h_valid_);
-  for (void* p : {(void*)keys_, (void*)vals_, (void*)keys_sorted_, (void*)vals_sorted_, (void*)bstart_, (void*)bend_,
-                  (void*)cnt_, (void*)off_task_, sort_tmp_, scan_tmp_, (void*)bcnt_, (void*)boff_, (void*)hist_,
-                  (void*)hoff_, (void*)nch_, (void*)choff_, (void*)hist2_, (void*)hoff2_, (void*)hs_hist_,
+  for (void* p : {(void*)vals_sorted_, (void*)bstart_, (void*)bend_, (void*)cnt_, (void*)off_task_, (void*)hs_hist_,
                   (void*)hs_blkoff_, (void*)hs_bintot_, (void*)hs_binbase_, (void*)hs_toff_, (void*)hs_hist2_,
                   (void*)hs_off2_, (void*)hs_subbase_, hs_ent_a_, hs_ent_b_, (void*)tsum_, (void*)perm_,
-                  (void*)tl_hist_, (void*)tl_off_, (void*)hs_toff3_, (void*)hs_hist3_, (void*)hs_off3_})
+                  (void*)tl_hist_, (void*)tl_off_, (void*)hs_toff3_, (void*)hs_hist3_, (void*)hs_off3_,
+                  (void*)lvl_all_, (void*)lvl_tsum_})
     if (p) (void)hipFree(p);
-  if (lvl_all_) (void)hipFree(lvl_all_);
-  if (lvl_tsum_) (void)hipFree(lvl_tsum_);
 }
 
 void MsmPlan::build(const uint32_t* scalars, size_t n) {
@@ -660,146 +311,73 @@ void MsmPlan::build(const uint32_t* scalars, size_t n) {
   const uint32_t W = (uint32_t)prm_.windows;
   const uint32_t nb = (uint32_t)nbuckets_;
   hipStream_t st = stream_;
-  total_ = 0;
-  bool counted = false;  // bucket bounds and task counts already written (k_hs_fine / k_hs_bounds3)
+  // total_ = n * W bounds the nonzero digits (the accumulate grid: threads past the last task exit),
+  // so nothing waits on the host; the exact count stays on the device (entries_dev)
+  total_ = (uint32_t)(n * W);
   hs_built_ = false;
-  if ((dense_ ? use_hsort_ : use_wsort_) && !use_bins_) {
-    // 1+2. hand-written three-pass LDS-staged bucket sort (hsort_kernels.hpp), zero digits dropped
-    // in pass A; total_ = n * W bounds the nonzero digits (the accumulate grid: threads past the last
-    // task exit), so nothing waits on the host; the exact count stays on the device (entries_dev)
-    total_ = (uint32_t)(n * W);
-    if (total_ == 0) {
-      HIPX(hipMemsetAsync(bstart_, 0, (nbuckets_ + 1) * 4, st));
-      HIPX(hipMemsetAsync(bend_, 0, (nbuckets_ + 1) * 4, st));
-    } else {
-      const int k = hs_k_;
-      const uint32_t nblk = (uint32_t)((n + k * HS_TPB - 1) / (k * HS_TPB)), nsub = 1u << hs_b2_;
-      const int sh1 = hs_b2_ + hs_b3_;
-      uint2* ea = static_cast<uint2*>(hs_ent_a_);
-      uint2* eb = static_cast<uint2*>(hs_ent_b_);
-      // A: digits -> bins
-      auto count1 = k == 4 ? k_hs_count1<4> : (k == 2 ? k_hs_count1<2> : k_hs_count1<1>);
-      hipLaunchKernelGGL(count1, dim3(nblk), dim3(HS_TPB), 0, st, scalars, (uint32_t)n, prm_.c, prm_.nb1, (int)W,
-                         prm_.depth, sh1, hs_nbins_, hs_hist_);
-      hipLaunchKernelGGL(k_hs_binscan, dim3(hs_nbins_), dim3(HS_TPB), 0, st, hs_hist_, nblk, hs_blkoff_, hs_bintot_);
-      hipLaunchKernelGGL(k_hs_binbase, dim3(1), dim3(512), 0, st, hs_bintot_, hs_nbins_, hs_binbase_, hs_toff_);
-      auto scatter1 = k == 4 ? k_hs_scatter1<4> : (k == 2 ? k_hs_scatter1<2> : k_hs_scatter1<1>);
-      const size_t lds1 = (size_t)k * HS_TPB * W * 8 + (size_t)hs_nbins_ * 8;
-      hipLaunchKernelGGL(scatter1, dim3(nblk), dim3(HS_TPB), lds1, st, scalars, (uint32_t)n, prm_.c, prm_.nb1, (int)W,
-                         prm_.depth, sh1, hs_nbins_, hs_blkoff_, hs_binbase_, ea);
-      // B: bins -> sub-bins (tiles past the used ones exit; their counters stay zero)
-      const size_t tiles = ((size_t)total_ + HS_TILE - 1) / HS_TILE + hs_nbins_;
-      const size_t nh2 = tiles << hs_b2_;
-      HIPX(hipMemsetAsync(hs_hist2_, 0, nh2 * 4, st));
-      const bool skew = !dense_;  // witness plans: whole waves of one bin / sub-bin / bucket
-      hipLaunchKernelGGL((skew ? k_hs_count2<true> : k_hs_count2<false>), dim3((unsigned)tiles), dim3(HS_TPB), 0, st,
-                         ea, hs_binbase_, hs_toff_, hs_nbins_, hs_b3_, nsub, hs_hist2_);
-      scan_nolookback(hs_hist2_, hs_off2_, nh2, tsum_, st);
-      const uint32_t nq = hs_nbins_ * nsub;
-      hipLaunchKernelGGL(k_hs_subbase, dim3(grid_for(nq + 1)), dim3(HS_TPB), 0, st, hs_off2_, hs_binbase_, hs_toff_,
-                         hs_nbins_, nsub, hs_subbase_);
-      hipLaunchKernelGGL((skew ? k_hs_scatter2<true, false> : k_hs_scatter2<false, false>), dim3((unsigned)tiles),
-                         dim3(HS_TPB), 0, st, ea, hs_binbase_, hs_toff_, hs_nbins_, hs_b3_, nsub, hs_off2_, eb,
-                         nullptr);
-      // C: sub-bins -> buckets, bounds and task counts
-      if (dense_ && !hs_tiled_c_) {
-        hipLaunchKernelGGL(k_hs_fine, dim3(nq), dim3(HS_FINE_TPB), 0, st, eb, hs_subbase_, nq, hs_b3_, nb,
-                           (uint32_t)prm_.S, vals_sorted_, bstart_, bend_, cnt_);
-      } else {  // tiled: pass B one level down (no workgroup takes more than HS_TILE entries)
-        const uint32_t nf = 1u << hs_b3_;
-        hipLaunchKernelGGL(k_hs_subtiles, dim3(1), dim3(SC_TPB), 0, st, hs_subbase_, nq, hs_toff3_);
-        const size_t tiles3 = ((size_t)total_ + HS_TILE - 1) / HS_TILE + nq, nh3 = tiles3 << hs_b3_;
-        HIPX(hipMemsetAsync(hs_hist3_, 0, nh3 * 4, st));
-        hipLaunchKernelGGL(k_hs_count2<true>, dim3((unsigned)tiles3), dim3(HS_TPB), 0, st, eb, hs_subbase_, hs_toff3_,
-                           nq, 0, nf, hs_hist3_);
-        scan_nolookback(hs_hist3_, hs_off3_, nh3, tsum_, st);
-        hipLaunchKernelGGL((k_hs_scatter2<true, true>), dim3((unsigned)tiles3), dim3(HS_TPB), 0, st, eb, hs_subbase_,
-                           hs_toff3_, nq, 0, nf, hs_off3_, nullptr, vals_sorted_);
-        hipLaunchKernelGGL(k_hs_bounds3, dim3(grid_for((size_t)nb + 1)), dim3(HS_TPB), 0, st, hs_toff3_, hs_off3_,
-                           hs_subbase_, hs_b3_, nb, (uint32_t)prm_.S, bstart_, bend_, cnt_);
-      }
-      counted = true;
-      hs_built_ = true;
-    }
-  } else if (dense_ && !use_bins_) {
-    // 1+2. dense digits (no compaction) and a full sort on the key bits + sentinel bit
+  if (total_ == 0) {
     HIPX(hipMemsetAsync(bstart_, 0, (nbuckets_ + 1) * 4, st));
     HIPX(hipMemsetAsync(bend_, 0, (nbuckets_ + 1) * 4, st));
-    total_ = (uint32_t)(n * W);
-    if (total_ > 0) {
-      hipLaunchKernelGGL(k_digit_write_dense, dim3(grid_for(n)), dim3(TPB), 0, st, scalars, (uint32_t)n, prm_.c,
-                         prm_.nb1, (int)W, prm_.depth, nb, keys_, vals_);
-      size_t tmp = sort_tmp_bytes_;
-      HIPX(sort_pairs(sort_tmp_, tmp, keys_, keys_sorted_, vals_, vals_sorted_, (size_t)total_, dense_bits_, st));
-      hipLaunchKernelGGL(k_bounds, dim3(grid_for(total_)), dim3(TPB), 0, st, keys_sorted_, total_, bstart_, bend_);
+    HIPX(hipMemsetAsync(cnt_, 0, (nbuckets_ + 1) * 4, st));
+  } else {
+    // the hand-written three-pass LDS-staged bucket sort (hsort_kernels.hpp), zero digits dropped in
+    // pass A.  Dense plans (uniform scalars: the H MSM) group their sub-bins with one workgroup each
+    // (k_hs_fine); compacted plans (the witness: whole waves of one bin / sub-bin / bucket) take the
+    // wave-aggregated LDS claims and the tiled pass C, as do keys with more than 5 bucket bits per
+    // sub-bin
+    const int k = hs_k_;
+    const uint32_t nblk = (uint32_t)((n + k * HS_TPB - 1) / (k * HS_TPB)), nsub = 1u << hs_b2_;
+    const int sh1 = hs_b2_ + hs_b3_;
+    uint2* ea = static_cast<uint2*>(hs_ent_a_);
+    uint2* eb = static_cast<uint2*>(hs_ent_b_);
+    // A: digits -> bins
+    auto count1 = k == 4 ? k_hs_count1<4> : (k == 2 ? k_hs_count1<2> : k_hs_count1<1>);
+    hipLaunchKernelGGL(count1, dim3(nblk), dim3(HS_TPB), 0, st, scalars, (uint32_t)n, prm_.c, (int)W, prm_.depth, sh1,
+                       hs_nbins_, hs_hist_);
+    hipLaunchKernelGGL(k_hs_binscan, dim3(hs_nbins_), dim3(HS_TPB), 0, st, hs_hist_, nblk, hs_blkoff_, hs_bintot_);
+    hipLaunchKernelGGL(k_hs_binbase, dim3(1), dim3(512), 0, st, hs_bintot_, hs_nbins_, hs_binbase_, hs_toff_);
+    auto scatter1 = k == 4 ? k_hs_scatter1<4> : (k == 2 ? k_hs_scatter1<2> : k_hs_scatter1<1>);
+    const size_t lds1 = (size_t)k * HS_TPB * W * 8 + (size_t)hs_nbins_ * 8;
+    hipLaunchKernelGGL(scatter1, dim3(nblk), dim3(HS_TPB), lds1, st, scalars, (uint32_t)n, prm_.c, (int)W, prm_.depth,
+                       sh1, hs_nbins_, hs_blkoff_, hs_binbase_, ea);
+    // B: bins -> sub-bins (tiles past the used ones exit; their counters stay zero)
+    const size_t tiles = ((size_t)total_ + HS_TILE - 1) / HS_TILE + hs_nbins_;
+    const size_t nh2 = tiles << hs_b2_;
+    HIPX(hipMemsetAsync(hs_hist2_, 0, nh2 * 4, st));
+    const bool skew = !dense_;
+    hipLaunchKernelGGL((skew ? k_hs_count2<true> : k_hs_count2<false>), dim3((unsigned)tiles), dim3(HS_TPB), 0, st, ea,
+                       hs_binbase_, hs_toff_, hs_nbins_, hs_b3_, nsub, hs_hist2_);
+    scan_nolookback(hs_hist2_, hs_off2_, nh2, tsum_, st);
+    const uint32_t nq = hs_nbins_ * nsub;
+    hipLaunchKernelGGL(k_hs_subbase, dim3(grid_for(nq + 1)), dim3(HS_TPB), 0, st, hs_off2_, hs_binbase_, hs_toff_,
+                       hs_nbins_, nsub, hs_subbase_);
+    hipLaunchKernelGGL((skew ? k_hs_scatter2<true, false> : k_hs_scatter2<false, false>), dim3((unsigned)tiles),
+                       dim3(HS_TPB), 0, st, ea, hs_binbase_, hs_toff_, hs_nbins_, hs_b3_, nsub, hs_off2_, eb, nullptr);
+    // C: sub-bins -> buckets, bounds and task counts
+    if (dense_ && hs_b3_ <= HS_B3) {
+      hipLaunchKernelGGL(k_hs_fine, dim3(nq), dim3(HS_FINE_TPB), 0, st, eb, hs_subbase_, nq, hs_b3_, nb,
+                         (uint32_t)prm_.S, vals_sorted_, bstart_, bend_, cnt_);
+    } else {  // tiled: pass B one level down (no workgroup takes more than HS_TILE entries)
+      const uint32_t nf = 1u << hs_b3_;
+      hipLaunchKernelGGL(k_hs_subtiles, dim3(1), dim3(SC_TPB), 0, st, hs_subbase_, nq, hs_toff3_);
+      const size_t tiles3 = ((size_t)total_ + HS_TILE - 1) / HS_TILE + nq, nh3 = tiles3 << hs_b3_;
+      HIPX(hipMemsetAsync(hs_hist3_, 0, nh3 * 4, st));
+      hipLaunchKernelGGL(k_hs_count2<true>, dim3((unsigned)tiles3), dim3(HS_TPB), 0, st, eb, hs_subbase_, hs_toff3_, nq,
+                         0, nf, hs_hist3_);
+      scan_nolookback(hs_hist3_, hs_off3_, nh3, tsum_, st);
+      hipLaunchKernelGGL((k_hs_scatter2<true, true>), dim3((unsigned)tiles3), dim3(HS_TPB), 0, st, eb, hs_subbase_,
+                         hs_toff3_, nq, 0, nf, hs_off3_, nullptr, vals_sorted_);
+      hipLaunchKernelGGL(k_hs_bounds3, dim3(grid_for((size_t)nb + 1)), dim3(HS_TPB), 0, st, hs_toff3_, hs_off3_,
+                         hs_subbase_, hs_b3_, nb, (uint32_t)prm_.S, bstart_, bend_, cnt_);
     }
-  } else if (use_bins_) {
-    // 1+2. bucket binning (k_bin_*, k_chunk_*): digits counted and scattered into coarse
-    //      bins, then each bin grouped by its fine key bits, bucket bounds on the way
-    HIPX(hipMemsetAsync(bstart_, 0, (nbuckets_ + 1) * 4, st));
-    HIPX(hipMemsetAsync(bend_, 0, (nbuckets_ + 1) * 4, st));
-    if (n > 0) {
-      const uint32_t nblk = grid_for(n, TPB * BIN_R);
-      const size_t nh = (size_t)nbins_ * nblk;
-      hipLaunchKernelGGL(k_bin_hist, dim3(nblk), dim3(TPB), 0, st, scalars, (uint32_t)n, prm_.c, prm_.nb1, (int)W,
-                         prm_.depth, fine_bits_, nbins_, hist_);
-      HIPX(hipMemsetAsync(hist_ + nh, 0, 4, st));
-      size_t stmp0 = scan_tmp_bytes_;
-      HIPX(hipcub::DeviceScan::ExclusiveSum(scan_tmp_, stmp0, hist_, hoff_, (int)(nh + 1), st));
-      hipLaunchKernelGGL(k_bin_scatter, dim3(nblk), dim3(TPB), 0, st, scalars, (uint32_t)n, prm_.c, prm_.nb1, (int)W,
-                         prm_.depth, fine_bits_, nbins_, hoff_, keys_, vals_);
-      hipLaunchKernelGGL(k_chunk_count, dim3(grid_for(nbins_ + 1)), dim3(TPB), 0, st, hoff_, nblk, nbins_, nch_);
-      size_t stmp1 = scan_tmp_bytes_;
-      HIPX(hipcub::DeviceScan::ExclusiveSum(scan_tmp_, stmp1, nch_, choff_, (int)(nbins_ + 1), st));
-      const size_t nh2 = (max_chunks_ << fine_bits_) + 1;  // unused tail stays zero
-      HIPX(hipMemsetAsync(hist2_, 0, nh2 * 4, st));
-      hipLaunchKernelGGL(k_chunk_hist, dim3((unsigned)max_chunks_), dim3(TPB), 0, st, keys_, hoff_, nblk, choff_,
-                         nbins_, fine_bits_, hist2_);
-      size_t stmp2 = scan_tmp_bytes_;
-      HIPX(hipcub::DeviceScan::ExclusiveSum(scan_tmp_, stmp2, hist2_, hoff2_, (int)nh2, st));
-      hipLaunchKernelGGL(k_chunk_scatter, dim3((unsigned)max_chunks_), dim3(TPB), 0, st, keys_, vals_, hoff_, nblk,
-                         choff_, nbins_, fine_bits_, hoff2_, vals_sorted_);
-      hipLaunchKernelGGL(k_chunk_bounds, dim3(grid_for(nbuckets_)), dim3(TPB), 0, st, choff_, fine_bits_, nb, hoff2_,
-                         bstart_, bend_);
-      HIPX(hipMemcpyAsync(h_valid_, hoff_ + nh, 4, hipMemcpyDeviceToHost, st));
-      HIPX(hipStreamSynchronize(st));
-      total_ = *h_valid_;
-    }
-  } else if (n > 0 && !use_wsort_) {
-    // 1. digits, compacted: only nonzero digits, window-major, point order within a window
-    const uint32_t nblk = grid_for(n);
-    hipLaunchKernelGGL(k_digit_count, dim3(nblk), dim3(TPB), 0, st, scalars, (uint32_t)n, prm_.c, prm_.nb1, (int)W,
-                       bcnt_);
-    HIPX(hipMemsetAsync(bcnt_ + (size_t)W * nblk, 0, 4, st));
-    size_t stmp0 = scan_tmp_bytes_;
-    HIPX(hipcub::DeviceScan::ExclusiveSum(scan_tmp_, stmp0, bcnt_, boff_, (int)((size_t)W * nblk + 1), st));
-    hipLaunchKernelGGL(k_digit_write, dim3(nblk), dim3(TPB), 0, st, scalars, (uint32_t)n, prm_.c, prm_.nb1, (int)W,
-                       prm_.depth, boff_, keys_, vals_);
-    HIPX(hipMemcpyAsync(h_valid_, boff_ + (size_t)W * nblk, 4, hipMemcpyDeviceToHost, st));
-    HIPX(hipStreamSynchronize(st));  // the sort needs the entry count on the host
-    total_ = *h_valid_;
+    hs_built_ = true;
   }
-  const bool compacted = !use_bins_ && !dense_ && !hs_built_ && !(use_wsort_ && n == 0);
-  if (compacted) {
-    HIPX(hipMemsetAsync(bstart_, 0, (nbuckets_ + 1) * 4, st));
-    HIPX(hipMemsetAsync(bend_, 0, (nbuckets_ + 1) * 4, st));
-  }
-  if (compacted && total_ > 0) {
-    // 2. stable LSD sort on the (c-1) bucket bits only: groups stay grouped (emission is
-    //    window-major), so equal (group, bucket) keys end up contiguous
-    size_t tmp = sort_tmp_bytes_;
-    HIPX(sort_pairs(sort_tmp_, tmp, keys_, keys_sorted_, vals_, vals_sorted_, (size_t)total_,
-                                            prm_.c - 1, st));
-    hipLaunchKernelGGL(k_bounds, dim3(grid_for(total_)), dim3(TPB), 0, st, keys_sorted_, total_, bstart_, bend_);
-  }
-  // 3. accumulate-task offsets and the heavy-bucket merge levels' offsets (look-back-free scans:
-  //    they run beside the accumulations of the other streams)
-  if (!counted)
-    hipLaunchKernelGGL(k_task_counts, dim3(grid_for(nbuckets_ + 1)), dim3(TPB), 0, st, bstart_, bend_, nb,
-                       (uint32_t)prm_.S, cnt_);
+  // accumulate-task offsets and the heavy-bucket merge levels' offsets (look-back-free scans: they
+  // run beside the accumulations of the other streams)
   scan_nolookback(cnt_, off_task_, nbuckets_ + 1, tsum_, st);
   max_tasks_now_ = ((size_t)total_ + prm_.S - 1) / prm_.S + nbuckets_;
-  if (use_perm_ && total_ > 0) {
+  if (total_ > 0) {
+    // accumulate-task order by length, longest first
     const unsigned nblk = grid_for(max_tasks_now_);
     const size_t lds = (size_t)(prm_.S + 1) * 4, nh = (size_t)(prm_.S + 1) * nblk;
     hipLaunchKernelGGL(k_tlen_count, dim3(nblk), dim3(TPB), lds, st, bstart_, bend_, off_task_, nb, (uint32_t)prm_.S,
@@ -836,8 +414,7 @@ MsmEngine::MsmEngine(Curve curve, const MsmParams& prm, size_t max_n, hipStream_
   HIPX(hipMalloc(&seg_s_, nseg * xyzz_words * 4));
   HIPX(hipMalloc(&seg_t_, nseg * xyzz_words * 4));
   const size_t n1 = (size_t)prm_.groups * prm_.K() *
-                    std::max(((half / prm_.M) + 2 * std::min<size_t>(prm_.L, msmk::TREE_CHAIN_FAN) - 1) /
-                                 (2 * std::min<size_t>(prm_.L, msmk::TREE_CHAIN_FAN)),
+                    std::max(((half / prm_.M) + 2 * msmk::TREE_CHAIN_FAN - 1) / (2 * msmk::TREE_CHAIN_FAN),
                              ((half / prm_.M) + 2 * msmk::TREE_TPB - 1) / (2 * msmk::TREE_TPB));
   for (int i = 0; i < 2; ++i) HIPX(hipMalloc(&sub_[i], n1 * xyzz_words * 4));
   for (auto& e : ev_) {
@@ -862,10 +439,12 @@ void MsmEngine::collect(Stats& s) {
   for (int i = 0; i < pending_; ++i) {
     float ms = 0;
     HIPX(hipEventElapsedTime(&ms, ev_[i][0], ev_[i][1]));
+    const uint32_t adds = h_total_dev_[i] ? h_counts_[MAX_PENDING + i] : h_total_[i];
     s.accumulate_ms += ms;
     s.launches += 1;
-    s.mixed_adds += h_total_dev_[i] ? h_counts_[MAX_PENDING + i] : h_total_[i];
+    s.mixed_adds += adds;
     s.tasks += h_counts_[i];
+    s.per_launch.push_back({ms, adds});
   }
   pending_ = 0;
 }
@@ -874,8 +453,8 @@ void MsmEngine::accumulate(const MsmPlan& plan, const MsmBases& bases) {
   const MsmParams& p = plan.params();
   if (p.c != prm_.c || p.depth != prm_.depth || p.windows != prm_.windows)
     throw std::runtime_error("MSM: plan and engine parameters differ");
-  if (bases.c() != p.c || bases.depth() != p.depth || bases.curve() != curve_ || bases.nb1() != p.nb1)
-    throw std::runtime_error("MSM: base table does not match the plan (c, depth, window widths, curve)");
+  if (bases.c() != p.c || bases.depth() != p.depth || bases.curve() != curve_)
+    throw std::runtime_error("MSM: base table does not match the plan (c, depth, curve)");
   if (bases.n() != plan.n()) throw std::runtime_error("MSM: base table size differs from the scalar count");
   if (plan.n() > max_n_) throw std::runtime_error("MSM: n exceeds engine capacity");
   HIPX(hipStreamWaitEvent(stream_, plan.ready(), 0));

@@ -14,13 +14,12 @@
 //
 //  MsmPlan   (per scalar vector, per proof; shared by every MSM over the same
 //     scalars -- A, B1, C and the G2 MSM B2 all use the witness)
-//     1. digits : compacted emission of the nonzero signed c-bit digits as
-//                 (key = group*2^(c-1) + |d|-1, val = (t*n + i) | sign<<31),
-//                 window-major, point order within a window.
-//     2. sort   : stable radix sort on the c-1 bucket bits (groups stay grouped).
+//     1. digits : the nonzero signed c-bit digits as (key = group*2^(c-1) + |d|-1,
+//                 val = (t*n + i) | sign<<31), computed from the scalars inside
+//     2. sort   : the hand-written three-pass LDS-staged bucket sort (hsort_kernels.hpp)
 //     3. bounds : bucket [start, end) ranges, accumulate-task offsets (tasks of
-//                 <= S entries never straddle a bucket) and the offsets of the
-//                 heavy-bucket merge levels.
+//                 <= S entries never straddle a bucket), the task order by length and
+//                 the offsets of the heavy-bucket merge levels.
 //
 //  MsmEngine (per curve and stream: partial sums, buckets, reduction tree)
 //     4. accumulate: one thread per task, mixed XYZZ additions of gathered bases;
@@ -38,6 +37,8 @@
 #include <hip/hip_runtime.h>
 #include <cstddef>
 #include <cstdint>
+#include <stdexcept>
+#include <string>
 #include <vector>
 
 namespace zkp {
@@ -50,33 +51,26 @@ struct MsmParams {
   int S = 32;        // max entries per accumulate task
   int S2 = 4;        // fan-in of a heavy-bucket merge level (short chains: latency-bound)
   int M = 4;         // buckets per reduction segment (running sums)
-  int L = 8;         // fan-in of a subset-sum tree level
-  int nb1 = 255;     // windows 0..nb1-1 are c bits wide, the rest c-1 (>= windows: all c bits)
-  // c_override / depth_override: 0 = automatic.  balanced (only with depth == windows, one bucket
-  // group): the W windows split the 255 digit bits as nb1 x c + (W - nb1) x (c - 1), so the top window
-  // is not a narrow one whose n digits pile into its few low buckets (c = 20: 8 x 20 + 5 x 19 bits
-  // instead of 12 x 20 + 15; the (c-1)-bit windows use the lower half of the shared buckets)
-  static MsmParams make(size_t n, int c_override = 0, int depth_override = 0, bool balanced = false) {
+  // c_override / depth_override: 0 = automatic.  Window bits must lie in [MIN_C, MAX_C]: W <= 32
+  // windows keep a scalar block's digits in one LDS stage of the bucket sort, and the bucket key
+  // (group and bucket bits, <= 27) splits into its three passes (hsort_kernels.hpp).
+  static constexpr int MIN_C = 8, MAX_C = 24;
+  static MsmParams make(size_t n, int c_override = 0, int depth_override = 0) {
     MsmParams p;
     int lg = 0;
     while ((size_t(1) << lg) < n) ++lg;
-    // one bucket set of 2^(c-1) buckets against n*W entries: c = lg - 3 keeps every
-    // bucket ~16*W entries deep and the bucket reduction (2^c full adds) < 2% of the
-    // accumulation; 20 bits caps the sort at three 8-bit passes.
-    p.c = c_override > 0 ? c_override : (lg - 4 < 8 ? 8 : (lg - 4 > 20 ? 20 : lg - 4));
-    if (p.c < 2) p.c = 2;
-    if (p.c > 24) p.c = 24;
+    // one bucket set of 2^(c-1) buckets against n*W entries: c = lg - 4 keeps every bucket ~8*W
+    // entries deep and the bucket reduction (2^c full adds) small; 20 bits caps the automatic choice
+    p.c = c_override > 0 ? c_override : (lg - 4 < MIN_C ? MIN_C : (lg - 4 > 20 ? 20 : lg - 4));
+    if (p.c < MIN_C || p.c > MAX_C)
+      throw std::invalid_argument("MSM window bits must be within " + std::to_string(MIN_C) + ".." +
+                                  std::to_string(MAX_C) + " (got " + std::to_string(p.c) + ")");
     p.windows = (255 + p.c - 1) / p.c;
     p.depth = depth_override > 0 ? (depth_override < p.windows ? depth_override : p.windows) : p.windows;
     p.groups = (p.windows + p.depth - 1) / p.depth;
     if (p.M > (1 << (p.c - 1))) p.M = 1 << (p.c - 1);
-    if (balanced && p.groups == 1 && p.c >= 3) {
-      const int nb = 255 - p.windows * (p.c - 1);
-      p.nb1 = nb < 0 ? 0 : (nb > p.windows ? p.windows : nb);
-    }
     return p;
   }
-  bool balanced() const { return nb1 < windows; }
   // reduction output: per group, lgP subset sums Q_b and sum_p T_p (P = 2^(c-1) / M segments)
   int lg_m() const { int l = 0; while ((1 << l) < M) ++l; return l; }
   int lgP() const { return c - 1 - lg_m(); }
@@ -111,7 +105,7 @@ inline int curve_fwords(Curve c) { return c == Curve::G1 ? 8 : 16; }
 // Precomputed base table: rows() x n affine points (device layout, Montgomery R'=2^261).
 class MsmBases {
  public:
-  MsmBases(Curve curve, size_t n, int c, int depth, int nb1 = 255);
+  MsmBases(Curve curve, size_t n, int c, int depth);
   ~MsmBases();
   MsmBases(const MsmBases&) = delete;
   MsmBases& operator=(const MsmBases&) = delete;
@@ -122,7 +116,6 @@ class MsmBases {
   size_t n() const { return n_; }
   int c() const { return c_; }
   int depth() const { return depth_; }
-  int nb1() const { return nb1_; }
   Curve curve() const { return curve_; }
   size_t bytes() const { return bytes_; }
   static size_t bytes_for(Curve curve, size_t n, int depth) {
@@ -132,7 +125,7 @@ class MsmBases {
  private:
   Curve curve_;
   size_t n_;
-  int c_, depth_, nb1_;
+  int c_, depth_;
   size_t bytes_ = 0;
   uint32_t* d_ = nullptr;
 };
@@ -145,13 +138,12 @@ class MsmPlan {
   MsmPlan& operator=(const MsmPlan&) = delete;
   // scalars: device, 8 LE 32-bit words each (standard form, any value < 2^256: reduced below r
   // when loaded, msm_kernels.hpp load_scalar, so W = ceil(255 / c) windows always hold the carry).
-  // Enqueues on the plan's stream and blocks the host once (the task grid needs the
-  // number of nonzero digits); records ready() at the end.  Grouping by bucket: a stable
-  // rocprim radix sort, or with ZKP_PLAN_SORT=bins a two-level counting sort (msm.hip).
+  // Enqueues on the plan's stream, never blocks the host (the exact entry count stays on the
+  // device: entries_dev()); records ready() at the end.
   void build(const uint32_t* scalars, size_t n);
-  // dense emission (for uniform scalars, e.g. the H MSM's): every (window, point) digit is an
-  // entry, zero digits keyed past the last bucket, so build() never blocks the host and the
-  // entry count is the bound n * W (entries() then counts the rare zero digits too)
+  // dense (uniform scalars, e.g. the H MSM's: nearly every digit is nonzero and the buckets evenly
+  // filled): pass C of the sort takes one workgroup per sub-bin; otherwise (the 0/1-heavy witness:
+  // whole waves of entries in one bucket) wave-aggregated LDS claims and a tiled pass C
   void set_dense(bool d) { dense_ = d; }
   bool dense() const { return dense_; }
   const MsmParams& params() const { return prm_; }
@@ -159,10 +151,9 @@ class MsmPlan {
   hipStream_t stream() const { return stream_; }
   size_t n() const { return n_; }
   size_t max_n() const { return max_n_; }
-  // entries the accumulate grid is sized for: the nonzero digits, or for the hand-sorted plans (whose
-  // count stays on the device: no host round trip) the bound n * W
+  // entries the accumulate grid is sized for: the bound n * W (the exact count stays on the device)
   uint32_t entries() const { return total_; }
-  // device word holding the exact nonzero-digit count once ready() (hand-sorted plans), else nullptr
+  // device word holding the exact nonzero-digit count once ready() (nullptr for an empty plan)
   const uint32_t* entries_dev() const { return hs_built_ ? hs_binbase_ + hs_nbins_ : nullptr; }
   int merge_levels() const { return merge_levels_; }
 
@@ -171,7 +162,7 @@ class MsmPlan {
   const uint32_t* bstart() const { return bstart_; }
   const uint32_t* bend() const { return bend_; }
   const uint32_t* task_off() const { return off_task_; }
-  const uint32_t* perm() const { return use_perm_ ? perm_ : nullptr; }  // task order (by length)
+  const uint32_t* perm() const { return perm_; }  // task order (by length)
   const uint32_t* level_off(int lv) const { return off_lvl_[lv]; }
   size_t max_tasks_now() const { return max_tasks_now_; }
   size_t max_tasks() const { return max_tasks_; }
@@ -184,28 +175,13 @@ class MsmPlan {
   size_t nbuckets_ = 0, max_entries_ = 0, max_tasks_ = 0, max_tasks_now_ = 0;
   int merge_levels_ = 0;
   uint32_t total_ = 0;
-  uint32_t *keys_ = nullptr, *vals_ = nullptr, *keys_sorted_ = nullptr, *vals_sorted_ = nullptr;
+  uint32_t *vals_sorted_ = nullptr;              // base|sign words in bucket order (the accumulation's input)
   uint32_t *bstart_ = nullptr, *bend_ = nullptr, *cnt_ = nullptr, *off_task_ = nullptr;
   std::vector<uint32_t*> off_lvl_;                // merge level l's offsets: lvl_all_ + l * (buckets + 1)
   uint32_t *lvl_all_ = nullptr, *lvl_tsum_ = nullptr;
-  uint32_t *bcnt_ = nullptr, *boff_ = nullptr;  // per (window, digit block) counts / offsets
-  // bucket binning (default grouping): coarse bins x binning blocks counts / offsets
-  bool use_bins_ = false;
   bool dense_ = false;
-  int dense_bits_ = 0;                          // key bits of the dense sort (sentinel = buckets)
-  int fine_bits_ = 0;
-  uint32_t nbins_ = 0;
-  uint32_t *hist_ = nullptr, *hoff_ = nullptr;
-  uint32_t *nch_ = nullptr, *choff_ = nullptr, *hist2_ = nullptr, *hoff2_ = nullptr;
-  size_t max_chunks_ = 0;
-  uint32_t* h_valid_ = nullptr;                 // pinned: number of nonzero digits
-  // dense plans: the hand-written three-pass LDS-staged bucket sort (hsort_kernels.hpp);
-  // ZKP_H_SORT=rocprim restores the onesweep radix sort of the sentinel-keyed digits
-  bool use_hsort_ = false;
-  // compacted (witness) plans sorted by the same passes (ZKP_W_SORT=rocprim: the onesweep sort and
-  // a host round trip for the entry count), always with the tiled pass C (skewed buckets); dense
-  // plans take the one-workgroup-per-sub-bin pass C unless ZKP_HS_TILED_C=1
-  bool use_wsort_ = false, hs_tiled_c_ = false, hs_built_ = false;
+  // the three-pass LDS-staged bucket sort (hsort_kernels.hpp)
+  bool hs_built_ = false;
   uint32_t hs_max_tiles3_ = 0;
   uint32_t *hs_toff3_ = nullptr, *hs_hist3_ = nullptr, *hs_off3_ = nullptr;
   int hs_b2_ = 0, hs_b3_ = 0, hs_k_ = 1;  // hs_k_: scalars per thread in pass A
@@ -213,15 +189,9 @@ class MsmPlan {
   uint32_t *hs_hist_ = nullptr, *hs_blkoff_ = nullptr, *hs_bintot_ = nullptr, *hs_binbase_ = nullptr;
   uint32_t *hs_toff_ = nullptr, *hs_hist2_ = nullptr, *hs_off2_ = nullptr, *hs_subbase_ = nullptr;
   void *hs_ent_a_ = nullptr, *hs_ent_b_ = nullptr;  // 8-byte (key, base|sign) entries
-  // accumulate-task order by length (ZKP_TASK_ORDER=bucket: bucket order)
-  bool use_perm_ = false;
+  // accumulate-task order by length (longest first)
   uint32_t *perm_ = nullptr, *tl_hist_ = nullptr, *tl_off_ = nullptr;
   uint32_t* tsum_ = nullptr;                    // tile sums of the look-back-free scans
-  size_t tsum_len_ = 0;
-  void* sort_tmp_ = nullptr;
-  size_t sort_tmp_bytes_ = 0;
-  void* scan_tmp_ = nullptr;
-  size_t scan_tmp_bytes_ = 0;
 };
 
 class MsmEngine {
@@ -247,11 +217,16 @@ class MsmEngine {
   // Kernel instrumentation (HIP events on this engine's stream).  When enabled,
   // every run() brackets the bucket-accumulate kernel with events; collect()
   // must be called after the stream is synchronised.
+  struct Launch {
+    float ms;       // HIP events on the engine's stream around the launch
+    uint32_t adds;  // nonzero digits it accumulated (mixed additions)
+  };
   struct Stats {
     double accumulate_ms = 0;  // summed over launches
     uint64_t launches = 0;
     uint64_t mixed_adds = 0;   // nonzero (point, window) digits processed
     uint64_t tasks = 0;
+    std::vector<Launch> per_launch;  // every collected launch, in order
   };
   void set_instrument(bool on) { instrument_ = on; }
   void collect(Stats& s);

@@ -1,7 +1,6 @@
 // Per-thread bodies of the MSM kernels (__host__ __device__ so that
 // tools/hosttest/msm_emu.cpp can replay the exact pipeline on the CPU).
 #pragma once
-#include <type_traits>
 #include "curve.hpp"
 
 namespace zkp {
@@ -35,18 +34,11 @@ ZDEV void load_scalar(const uint32_t* __restrict__ scalars, uint32_t i, uint32_t
   while (scalar_geq_r(s)) scalar_sub_r(s);
 }
 
-// Window geometry: windows 0..nb1-1 are c bits wide, windows nb1.. are c-1 bits wide (nb1 >= W:
-// all c bits, the default).  "Balanced" widths (MsmParams::balanced) spread the 255 digit bits
-// evenly instead of leaving a narrow top window whose digits all fall into a few low buckets.
-ZDEV int win_bit(int w, int c, int nb1) { return w < nb1 ? w * c : nb1 * c + (w - nb1) * (c - 1); }
-ZDEV int win_width(int w, int c, int nb1) { return w < nb1 ? c : c - 1; }
-
-// signed digit of window w (windows visited in order, carry threaded through):
+// signed c-bit digit of window w (windows visited in order, carry threaded through):
 // returns |d| (0 for a zero digit); neg = (d < 0)
-ZDEV uint32_t digit_mag(const uint32_t (&s)[9], int w, int c, int nb1, uint32_t& carry, bool& neg) {
-  const int wb = win_width(w, c, nb1);
-  const uint32_t half = 1u << (wb - 1), full = 1u << wb;
-  const int bit = win_bit(w, c, nb1), j = bit >> 5, sh = bit & 31;
+ZDEV uint32_t digit_mag(const uint32_t (&s)[9], int w, int c, uint32_t& carry, bool& neg) {
+  const uint32_t half = 1u << (c - 1), full = 1u << c;
+  const int bit = w * c, j = bit >> 5, sh = bit & 31;
   const uint64_t v = (uint64_t)s[j] | ((uint64_t)s[j + 1] << 32);  // sh + c <= 31 + 24 < 64
   const uint32_t raw = ((uint32_t)(v >> sh) & (full - 1)) + carry;
   if (raw > half) {
@@ -60,19 +52,19 @@ ZDEV uint32_t digit_mag(const uint32_t (&s)[9], int w, int c, int nb1, uint32_t&
 }
 
 // entry of window w of scalar i: bucket key = group*2^(c-1) + |d|-1 with group = w / T,
-// base index (t*n + i) | sign with t = w % T (row t of the table holds 2^(bit offset of window t) P_i)
-ZDEV bool digit_entry(const uint32_t (&s)[9], int w, int c, int nb1, int T, uint32_t n, uint32_t i,
-                      uint32_t& carry, uint32_t& key, uint32_t& val) {
+// base index (t*n + i) | sign with t = w % T (row t of the table holds 2^(c t) P_i)
+ZDEV bool digit_entry(const uint32_t (&s)[9], int w, int c, int T, uint32_t n, uint32_t i, uint32_t& carry,
+                      uint32_t& key, uint32_t& val) {
   bool neg;
-  const uint32_t mag = digit_mag(s, w, c, nb1, carry, neg);
+  const uint32_t mag = digit_mag(s, w, c, carry, neg);
   const uint32_t g = (uint32_t)w / (uint32_t)T, t = (uint32_t)w - g * (uint32_t)T;
   key = (g << (c - 1)) + mag - 1;
   val = (t * n + i) | (neg ? 0x80000000u : 0u);
   return mag != 0;
 }
 
-// row t of base i from row t-1: 2^dbl * P, dbl = the width of window t - 1 (affine; infinity
-// stays all-zero)
+// row t of base i from row t-1: 2^dbl * P, dbl = the window width c (affine; infinity stays
+// all-zero)
 template <class F>
 ZDEV void extend_row(uint32_t i, uint32_t* __restrict__ table, uint32_t n, int dbl, int t) {
   if (i >= n) return;
@@ -84,21 +76,6 @@ ZDEV void extend_row(uint32_t i, uint32_t* __restrict__ table, uint32_t n, int d
     a = xyzz_to_aff(q);
   }
   store_aff(table, (size_t)t * n + i, a);
-}
-
-ZDEV void bounds(uint32_t i, const uint32_t* __restrict__ keys, uint32_t total, uint32_t* __restrict__ start,
-                uint32_t* __restrict__ end) {
-  if (i >= total) return;
-  const uint32_t k = keys[i];
-  if (i == 0 || keys[i - 1] != k) start[k] = i;
-  if (i == total - 1 || keys[i + 1] != k) end[k] = i + 1;
-}
-
-// cnt[b] = ceil((end[b]-start[b]) / S) for b < nb, cnt[nb] = 0
-ZDEV void task_counts(uint32_t b, const uint32_t* __restrict__ start, const uint32_t* __restrict__ end, uint32_t nb,
-                     uint32_t S, uint32_t* __restrict__ cnt) {
-  if (b > nb) return;
-  cnt[b] = b == nb ? 0u : (end[b] - start[b] + S - 1) / S;
 }
 
 // largest b in [0, nb) with off[b] <= t   (off[0] = 0 <= t < off[nb])
@@ -122,10 +99,6 @@ ZDEV uint32_t task_len(uint32_t t, const uint32_t* __restrict__ start, const uin
   return umin(end[b], s0 + S) - s0;
 }
 
-#ifndef ZKP_ACC_VALS_AHEAD
-#define ZKP_ACC_VALS_AHEAD 1
-#endif
-
 // the field the accumulation computes in: G1 with product columns as asm mad chains (consts.hpp
 // FqAccCfg: same values and storage, the 4-wave accumulation hides their wait states), G2 as is
 template <class F>
@@ -137,14 +110,11 @@ struct AccField<Fq> {
   using type = Fe<FqAccCfg>;
 };
 
-// the field of the merge and reduction kernels (full XYZZ additions, latency-bound chains):
-// ZKP_MERGE_CHAIN=1 gives them the accumulation's chained columns and lockstep product pairs
-#ifndef ZKP_MERGE_CHAIN
-#define ZKP_MERGE_CHAIN 1
-#endif
+// the field of the merge and reduction kernels (full XYZZ additions, latency-bound chains): the
+// accumulation's chained columns and lockstep product pairs (profiles/merge_chain_r03.txt)
 template <class F>
 struct MergeField {
-  using type = typename std::conditional<ZKP_MERGE_CHAIN != 0, typename AccField<F>::type, F>::type;
+  using type = typename AccField<F>::type;
 };
 
 // thread i runs task perm[i] (tasks ordered by length, longest first: the lanes of a wave run
@@ -168,22 +138,13 @@ ZDEV void accumulate(uint32_t i, const uint32_t* __restrict__ points, const uint
                              load_aff<F>(points, v1 & 0x7fffffffu), (v1 >> 31) != 0);
     j = s0 + 2;
   }
-#if ZKP_ACC_VALS_AHEAD
   // the next entry's index is loaded one addition ahead: each iteration then waits on one
   // memory latency (its base gather) instead of two dependent ones (index, then base)
   uint32_t vn = j < s1 ? vals[j] : 0u;
   for (; j < s1; ++j) {
     const uint32_t v = vn;
     if (j + 1 < s1) vn = vals[j + 1];
-#else
-  for (; j < s1; ++j) {
-    const uint32_t v = vals[j];
-#endif
-#ifdef ZKP_ACC_GATHER_MASK  // latency probe only (wrong results): gathers confined to a cache-resident slice
-    xyzz_add_aff(acc, load_aff<F>(points, v & ZKP_ACC_GATHER_MASK), (v >> 31) != 0);
-#else
     xyzz_add_aff(acc, load_aff<F>(points, v & 0x7fffffffu), (v >> 31) != 0);
-#endif
   }
   store_xyzz(out, t, acc);
 }
@@ -305,20 +266,7 @@ ZDEV void subset_first(uint32_t id, const uint32_t* __restrict__ s_in, const uin
   store_xyzz(out, id, acc);
 }
 
-// next level: nseg segments of n_in values -> n_out = ceil(n_in / fan) sums of fan consecutive
-template <class FS>
-ZDEV void subset_level(uint32_t id, const uint32_t* __restrict__ in, uint32_t nseg, uint32_t n_in, uint32_t fan,
-                       uint32_t* __restrict__ out) {
-  using F = typename MergeField<FS>::type;
-  const uint32_t n_out = (n_in + fan - 1) / fan;
-  if (id >= nseg * n_out) return;
-  const uint32_t seg = id / n_out, j = id - seg * n_out;
-  Xyzz<F> acc = xyzz_inf<F>();
-  for (uint32_t i = j * fan; i < umin((j + 1) * fan, n_in); ++i) xyzz_add(acc, load_xyzz<F>(in, (size_t)seg * n_in + i));
-  store_xyzz(out, id, acc);
-}
-
-// ---- subset sums by workgroup LDS trees (ZKP_SUBSET_TREE, default): a workgroup of TREE_TPB
+// ---- subset sums by workgroup LDS trees: a workgroup of TREE_TPB
 // threads sums 2 * TREE_TPB consecutive values of one sum -- two loads and one addition per
 // thread, then log2(TREE_TPB) halving levels through LDS -- so the sequential chain of a sum
 // over P/2 values is ~1 + 8 additions per launch and ceil(log_512(P/2)) launches, instead of

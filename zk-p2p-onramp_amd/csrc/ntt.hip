@@ -1,7 +1,6 @@
 // Fr NTT engine (see ntt.hpp for the algorithm).
 #include "ntt.hpp"
 
-#include <cstdlib>
 #include <stdexcept>
 
 #include "field.hpp"
@@ -16,30 +15,11 @@ constexpr int TPB = 256;
 constexpr int LOG_TILE = 10;  // elements per workgroup tile (1024, 36 KiB of LDS)
 constexpr int LOC_LOG = 10;   // local-root table: w_1024^e, e < 512
 constexpr int MAX_PASS_BITS = 8;
-// Radix-4 unit variant (A/B build knobs): ZKP_NTT_MUL2 = 1 computes y2, y3 as lazily reduced sums of
-// products with combined roots (field.hpp r4_dif, full-circle root table), 0 the four-multiply unit
-// (half-circle table); ZKP_NTT_PACKED = 1 keeps the LDS roots as 8 packed words (unpacked per use);
-// ZKP_NTT_WPE bounds the waves per SIMD the register allocation targets (0 = compiler's choice).
-#ifndef ZKP_NTT_MUL2
-#define ZKP_NTT_MUL2 0
-#endif
-#ifndef ZKP_NTT_PACKED
-#define ZKP_NTT_PACKED 0
-#endif
-#ifndef ZKP_NTT_WPE
-#define ZKP_NTT_WPE 0
-#endif
-// ZKP_NTT_SHOUP = 1: the stage-root products of the LDS stages are Shoup products by constants
-// (field.hpp mul_shoup: 143 mads, no per-column quotient digits) with each root's quotient staged
-// beside it in LDS; their outputs are < 3m, so the differences that take them use sub4.
-#ifndef ZKP_NTT_SHOUP
-#define ZKP_NTT_SHOUP 1
-#endif
-#if ZKP_NTT_SHOUP && (ZKP_NTT_MUL2 || ZKP_NTT_PACKED)
-#error "ZKP_NTT_SHOUP needs the four-multiply unit with unpacked roots"
-#endif
-constexpr int MAX_TW = ZKP_NTT_MUL2 ? (1 << MAX_PASS_BITS) : (1 << (MAX_PASS_BITS - 1));  // stage roots, b <= 8
-constexpr int RW = ZKP_NTT_SHOUP ? 2 * NL : (ZKP_NTT_PACKED ? 8 : NL);  // LDS words per root
+constexpr int MAX_TW = 1 << (MAX_PASS_BITS - 1);  // stage roots w_(2^b)^j, j < 2^(b-1), b <= 8
+// the stage-root products are Shoup products by constants (field.hpp mul_shoup: 143 mads, no per-column
+// quotient digits): each root's plain limbs and its quotient floor(w 2^261 / r) are staged in LDS
+// (2 x 9 words per root); their outputs are < 3m, so the differences that take them use sub4
+constexpr int RW = 2 * NL;  // LDS words per root
 
 
 __device__ __forceinline__ uint32_t brev(uint32_t x, int b) { return __builtin_bitreverse32(x) >> (32 - b); }
@@ -59,55 +39,16 @@ struct Tile {
   int lm, b, lc, lbt;
 };
 
-// the stage roots w_(2^b)^j staged in LDS (SoA): j < 2^(b-1), and with ZKP_NTT_MUL2 the full
-// circle j < 2^b (w^(j + 2^(b-1)) = -w^j: the combined roots of r4_dif reach every exponent)
-__device__ __forceinline__ void put_root(uint32_t* __restrict__ ltw, int j, const Fr& x) {
-#if ZKP_NTT_PACKED
-  uint32_t w[8];
-  pack(x, w);
-#pragma unroll
-  for (int l = 0; l < 8; ++l) ltw[l * MAX_TW + j] = w[l];
-#else
-#pragma unroll
-  for (int l = 0; l < NL; ++l) ltw[l * MAX_TW + j] = x.v[l];
-#endif
-}
-// the stage roots of a b-bit pass staged in LDS from the w_1024 table, in every workgroup
-__device__ __forceinline__ void stage_roots_loc(uint32_t* __restrict__ ltw, const uint32_t* __restrict__ loc, int b) {
-  const int TW = 1 << (b - 1);
-  for (int j = threadIdx.x; j < TW; j += TPB) {
-    const Fr x = load_fe<FrCfg>(loc + (size_t)(j << (LOC_LOG - b)) * 8);  // canonical Montgomery form
-#if ZKP_NTT_SHOUP
-    // plain root w (limbs 0..8) and its Shoup quotient floor(w 2^261 / r) (limbs 9..17)
-    const Fr w = from_mont(x), wq = shoup_quot(x);
-#pragma unroll
-    for (int l = 0; l < NL; ++l) {
-      ltw[l * MAX_TW + j] = w.v[l];
-      ltw[(NL + l) * MAX_TW + j] = wq.v[l];
-    }
-#else
-    put_root(ltw, j, x);
-    if (ZKP_NTT_MUL2) put_root(ltw, j + TW, neg(x));
-#endif
-  }
-}
-
-// Shoup builds: the roots precomputed once per (direction, b) in their LDS layout (k_root_table),
-// so staging is a copy instead of two products per root per workgroup (~4 % of a pass's
-// multiplies); rtab == nullptr (ZKP_NTT_RTAB=0) stages them from the w_1024 table
-__device__ __forceinline__ void stage_roots(uint32_t* __restrict__ ltw, const uint32_t* __restrict__ rtab,
-                                            const uint32_t* __restrict__ loc, int b) {
-  if (!ZKP_NTT_SHOUP || !rtab) {
-    stage_roots_loc(ltw, loc, b);
-    return;
-  }
+// the stage roots of a b-bit pass, precomputed once per (direction, b) in their LDS layout
+// (k_root_table): staging is a copy (no products per root per workgroup)
+__device__ __forceinline__ void stage_roots(uint32_t* __restrict__ ltw, const uint32_t* __restrict__ rtab) {
   const uint4* s = reinterpret_cast<const uint4*>(rtab);
   uint4* d = reinterpret_cast<uint4*>(ltw);
   for (int k = threadIdx.x; k < RW * MAX_TW / 4; k += TPB) d[k] = s[k];
 }
 
-#if ZKP_NTT_SHOUP
-// rtab in the LDS layout of stage_roots: ltw[l * MAX_TW + j], j < 2^(b-1) (the rest zero)
+// rtab in the LDS layout of stage_roots: ltw[l * MAX_TW + j] = limb l of the plain root w_(2^b)^j,
+// ltw[(NL + l) * MAX_TW + j] = limb l of its Shoup quotient, j < 2^(b-1) (the rest zero)
 __global__ __launch_bounds__(TPB) void k_root_table(uint32_t* __restrict__ rtab, const uint32_t* __restrict__ loc, int b) {
   const int j = blockIdx.x * TPB + threadIdx.x;
   if (j >= MAX_TW) return;
@@ -123,7 +64,6 @@ __global__ __launch_bounds__(TPB) void k_root_table(uint32_t* __restrict__ rtab,
     rtab[(NL + l) * MAX_TW + j] = wq.v[l];
   }
 }
-#endif
 
 // LDS data-tile swizzle: element e lives at word e ^ S(e), S(e) = (h ^ 2h ^ 8h) mod 32, h = e >> 5
 // (an XOR of bits 5.. into the bank bits 0..4).  ds_read_b32 / ds_write_b32 banks are word mod 32 per
@@ -154,48 +94,10 @@ __device__ __forceinline__ void lds_put(uint32_t* __restrict__ lds, int E_rt, in
 #pragma unroll
   for (int l = 0; l < NL; ++l) lds[l * E + e] = x.v[l];
 }
-__device__ __forceinline__ Fr root(const uint32_t* __restrict__ ltw, uint32_t j) {
-#if ZKP_NTT_PACKED
-  uint32_t w[8];
-#pragma unroll
-  for (int l = 0; l < 8; ++l) w[l] = ltw[l * MAX_TW + j];
-  return unpack<FrCfg>(w);
-#else
-  Fr w;
-#pragma unroll
-  for (int l = 0; l < NL; ++l) w.v[l] = ltw[l * MAX_TW + j];
-  return w;
-#endif
-}
-// a * w_j for a stage root: a Shoup product (output < 3m) or a Montgomery one (< 2m)
-__device__ __forceinline__ Fr root_mul(const Fr& a, const uint32_t* __restrict__ ltw, uint32_t j) {
-#if ZKP_NTT_SHOUP
-  Fr w, wq;
-#pragma unroll
-  for (int l = 0; l < NL; ++l) {
-    w.v[l] = ltw[l * MAX_TW + j];
-    wq.v[l] = ltw[(NL + l) * MAX_TW + j];
-  }
-  return mul_shoup(a, w, wq);
-#else
-  return mul(a, root(ltw, j));
-#endif
-}
-// x - y for stage values (< 3m with Shoup products, else < 2m)
-__device__ __forceinline__ Fr stage_sub(const Fr& x, const Fr& y) { return ZKP_NTT_SHOUP ? sub4(x, y) : sub(x, y); }
-// DIF butterfly output d = (x - y) w_j, with w_0 = 1 (x - y only feeds the multiply: raw)
-__device__ __forceinline__ Fr bfly_d(const Fr& x, const Fr& y, const uint32_t* __restrict__ ltw, uint32_t j) {
-  return j ? root_mul(rsub(x, y), ltw, j) : stage_sub(x, y);
-}
-// ZKP_NTT_PAIRS (Shoup builds, default on): a * w_ja and c * w_jc as one lockstep pair of Shoup
-// products (field.hpp mul_shoup_pair; with Fr's chained columns the two chains fill each other's
-// wait states); outputs < 3m
-#ifndef ZKP_NTT_PAIRS
-#define ZKP_NTT_PAIRS ZKP_NTT_SHOUP
-#endif
-#if ZKP_NTT_PAIRS && (!ZKP_NTT_SHOUP || ZKP_NTT_MUL2)
-#error "ZKP_NTT_PAIRS needs the Shoup four-multiply unit"
-#endif
+// x - y for stage values (Shoup products: < 3m)
+__device__ __forceinline__ Fr stage_sub(const Fr& x, const Fr& y) { return sub4(x, y); }
+// a * w_ja and c * w_jc as one lockstep pair of Shoup products (field.hpp mul_shoup_pair; with Fr's
+// chained columns the two chains fill each other's wait states); outputs < 3m
 __device__ __forceinline__ void root_mul_pair(const Fr& a, uint32_t ja, const Fr& c, uint32_t jc,
                                               const uint32_t* __restrict__ ltw, Fr& r, Fr& s) {
   Fr w, wq, v, vq;
@@ -229,31 +131,6 @@ __device__ __forceinline__ void r4_unit(uint32_t* __restrict__ lds, const uint32
            x3 = lds_get<LE>(lds, E, p3);
   // stage t: (x0, x2) with w_(2H)^i, (x1, x3) with w_(2H)^(i + H/2); stage t+1: (s02, s13)
   // and (d02, d13), both with w_H^i.  Roots as exponents of w_(2^b) (stage t: i << t).
-#if ZKP_NTT_MUL2
-  if (Hh > 1) {
-    // y0 = s02 + s13 and y1 = (s02 - s13) w_H^i with the sums raw (< 4m, one reduction);
-    // y2 = d02 + d13 and y3 = (d02 - d13) w_H^i as lazily reduced sums of products over
-    // u = x0 - x2 and v = x1 - x3 with combined roots (r4_dif): 3 reductions per unit, not 4
-    const uint32_t ia = i << t, ib = (i + Hh) << t, ic = (3 * i) << t;
-    const uint32_t id = ((3 * i + 3 * Hh) << t) & ((1u << b) - 1);  // -w^(3i + H/2) = w^(3i + 3H/2)
-    Fr y0, y1, y2, y3;
-    r4_dif(x0, x1, x2, x3, root(ltw, ia), root(ltw, ib), root(ltw, ic), root(ltw, id), root(ltw, i << (t + 1)), y0,
-           y1, y2, y3);
-    lds_put<LE>(lds, E, p0, y0);
-    lds_put<LE>(lds, E, p1, y1);
-    lds_put<LE>(lds, E, p2, y2);
-    lds_put<LE>(lds, E, p3, y3);
-  } else {  // last pair (span 1, i = 0): roots 1 except w_(2H)^(H/2) for (x1, x3)
-    const Fr d02 = sub(x0, x2);
-    const Fr d13 = mul(rsub(x1, x3), root(ltw, Hh << t));
-    const Fr s02 = add(x0, x2), s13 = add(x1, x3);
-    lds_put<LE>(lds, E, p0, add(s02, s13));
-    lds_put<LE>(lds, E, p1, sub(s02, s13));
-    lds_put<LE>(lds, E, p2, add(d02, d13));
-    lds_put<LE>(lds, E, p3, sub(d02, d13));
-  }
-#else
-#if ZKP_NTT_PAIRS
   // the unit's independent root products in lockstep pairs (d02 / d13, then y1 / y3 by the same
   // root); every lane multiplies (w^0 = 1 for i = 0: no divergent j == 0 path)
   const uint32_t j = i << (t + 1);
@@ -273,23 +150,6 @@ __device__ __forceinline__ void r4_unit(uint32_t* __restrict__ lds, const uint32
     lds_put<LE>(lds, E, p3, stage_sub(d02, d13));
   }
   lds_put<LE>(lds, E, p2, add(d02, d13));
-#else
-  const Fr d02 = bfly_d(x0, x2, ltw, i << t);
-  const Fr d13 = bfly_d(x1, x3, ltw, (i + Hh) << t);
-  const uint32_t j = i << (t + 1);
-  if (Hh > 1) {  // the sums stay raw (< 4m) and meet one reduction; w_H^0 = 1 (Montgomery) for i = 0
-    const Fr s02 = add_raw(x0, x2), s13 = add_raw(x1, x3);
-    lds_put<LE>(lds, E, p0, add_raw_reduce(s02, s13));
-    lds_put<LE>(lds, E, p1, root_mul(sub_raw6(s02, s13), ltw, j));
-  } else {  // last pair (span 1): no multiply in stage t+1
-    const Fr s02 = add(x0, x2), s13 = add(x1, x3);
-    lds_put<LE>(lds, E, p0, add(s02, s13));
-    lds_put<LE>(lds, E, p1, sub(s02, s13));
-  }
-  lds_put<LE>(lds, E, p2, add(d02, d13));
-  lds_put<LE>(lds, E, p3, bfly_d(d02, d13, ltw, j));
-#endif
-#endif
 }
 
 // b radix-2 DIF stages on the LDS tile (rows natural in, bit-reversed out), done two at a
@@ -348,22 +208,16 @@ __device__ __forceinline__ int brev_src(const Tile& T, int e) {
 // 2: the fused innermost pair of coset_extend (lm == b): inverse-root DFT, coset key
 //    (table by digit-reversed position), forward-root DFT on one LDS-resident tile.
 // tw: w_(2^lm)^(col*row) by position in block (null when n2 == 1).  rootsA / rootsB: the stage
-// roots (Shoup builds: the k_root_table of this b; else the w_1024 table), B for MODE 2's forward DFT.
-#if ZKP_NTT_WPE
-#define NTT_WPE_ATTR __attribute__((amdgpu_waves_per_eu(ZKP_NTT_WPE)))
-#else
-#define NTT_WPE_ATTR
-#endif
+// roots (the k_root_table of this b and direction), B for MODE 2's forward DFT.
 template <int MODE, int LE>
-__global__ __launch_bounds__(TPB) NTT_WPE_ATTR void k_ntt(uint32_t* __restrict__ data, Tile T, const uint32_t* __restrict__ tw,
+__global__ __launch_bounds__(TPB) void k_ntt(uint32_t* __restrict__ data, Tile T, const uint32_t* __restrict__ tw,
                                              const uint32_t* __restrict__ rootsA, const uint32_t* __restrict__ rootsB,
-                                             const uint32_t* __restrict__ locA, const uint32_t* __restrict__ locB,
                                              const uint32_t* __restrict__ coset) {
   __shared__ uint32_t lds[NL << LOG_TILE];  // SoA: lds[limb * E + element]
   __shared__ __attribute__((aligned(16))) uint32_t ltw[RW * MAX_TW];
   const int E = LE ? (1 << LE) : (1 << (T.b + T.lc + T.lbt));  // LE: the tile size known at compile time
   const uint32_t tile = blockIdx.x;
-  stage_roots(ltw, rootsA, locA, T.b);
+  stage_roots(ltw, rootsA);
   constexpr int VPT = (1 << LOG_TILE) / TPB;  // elements per thread of a full tile
   if (LE && MODE == 1 && tw) {
     // full tiles: the twiddle products of two elements at a time in lockstep (mul_pair)
@@ -436,7 +290,7 @@ __global__ __launch_bounds__(TPB) NTT_WPE_ATTR void k_ntt(uint32_t* __restrict__
       }
     }
     __syncthreads();
-    stage_roots(ltw, rootsB, locB, T.b);  // the forward roots replace the inverse ones (no reader until the next barrier)
+    stage_roots(ltw, rootsB);  // the forward roots replace the inverse ones (no reader until the next barrier)
 #pragma unroll
     for (int it = 0; it < VPT; ++it) {
       const int e = (int)threadIdx.x + it * TPB;
@@ -643,13 +497,7 @@ NttEngine::NttEngine(int log_n, hipStream_t stream) : log_n_(log_n), stream_(str
   coset_lo_ = upload_powers(g, nlo, 1, ninv, stream_);
   coset_hi_ = upload_powers(g, nhi, nlo, one, stream_);
   ninv_ = upload_powers(one, 1, 1, ninv, stream_);
-#if ZKP_NTT_SHOUP
-  // stage-root tables per (direction, pass bits) in the kernels' LDS layout (k_root_table);
-  // ZKP_NTT_RTAB=0 stages them from the w_1024 table in every workgroup instead (A/B knob)
-  {
-    const char* e = std::getenv("ZKP_NTT_RTAB");
-    use_rtab_ = !(e && std::atoi(e) == 0);
-  }
+  // stage-root tables per (direction, pass bits) in the kernels' LDS layout (k_root_table)
   for (int dir = 0; dir < 2; ++dir)
     for (int b : bits_)
       if (!rtab_[dir][b]) {
@@ -657,7 +505,6 @@ NttEngine::NttEngine(int log_n, hipStream_t stream) : log_n_(log_n), stream_(str
         hipLaunchKernelGGL(k_root_table, dim3((MAX_TW + TPB - 1) / TPB), dim3(TPB), 0, stream_, rtab_[dir][b],
                            loc_[dir], b);
       }
-#endif
   // per-pass twiddle tables (one multiply per element instead of lo*hi per element) and
   // the coset key by digit-reversed position: ~3 n x 32 B of HBM
   for (int dir = 0; dir < 2; ++dir) {
@@ -701,9 +548,7 @@ void NttEngine::launch_pass(uint32_t* data, int mode, int p, bool inv) {
   const Tile T = make_tile(k, lms_[p], bits_[p]);
   const size_t tiles = (size_t(1) << k) >> (T.b + T.lc + T.lbt);
   const int d = inv ? 1 : 0;
-  const bool rt = use_rtab_;
-  const uint32_t *ra = rt ? rtab_[d][T.b] : nullptr, *rinv = rt ? rtab_[1][T.b] : nullptr,
-                 *rfwd = rt ? rtab_[0][T.b] : nullptr;
+  const uint32_t *ra = rtab_[d][T.b], *rinv = rtab_[1][T.b], *rfwd = rtab_[0][T.b];
   const uint32_t* none = nullptr;
   // full 1024-element tiles (every transform of 2^10 points or more) take the compile-time tile size
   const bool full = T.b + T.lc + T.lbt == LOG_TILE;
@@ -711,14 +556,11 @@ void NttEngine::launch_pass(uint32_t* data, int mode, int p, bool inv) {
   auto k1 = full ? k_ntt<1, LOG_TILE> : k_ntt<1, 0>;
   auto k2 = full ? k_ntt<2, LOG_TILE> : k_ntt<2, 0>;
   if (mode == 0)
-    hipLaunchKernelGGL(k0, dim3((unsigned)tiles), dim3(TPB), 0, stream_, data, T, tw_pass_[d][p], ra, none, loc_[d],
-                       none, none);
+    hipLaunchKernelGGL(k0, dim3((unsigned)tiles), dim3(TPB), 0, stream_, data, T, tw_pass_[d][p], ra, none, none);
   else if (mode == 1)
-    hipLaunchKernelGGL(k1, dim3((unsigned)tiles), dim3(TPB), 0, stream_, data, T, tw_pass_[d][p], ra, none, loc_[d],
-                       none, none);
+    hipLaunchKernelGGL(k1, dim3((unsigned)tiles), dim3(TPB), 0, stream_, data, T, tw_pass_[d][p], ra, none, none);
   else
-    hipLaunchKernelGGL(k2, dim3((unsigned)tiles), dim3(TPB), 0, stream_, data, T, none, rinv, rfwd, loc_[1], loc_[0],
-                       coset_pos_);
+    hipLaunchKernelGGL(k2, dim3((unsigned)tiles), dim3(TPB), 0, stream_, data, T, none, rinv, rfwd, coset_pos_);
 }
 
 void NttEngine::dif_passes(uint32_t* data, bool inv, int first, int last) {

@@ -61,7 +61,6 @@ class NttEngine {
   std::vector<uint32_t*> tw_pass_[2];      // per DIF pass p: w_(2^lm)^(col*row) by position in block (null: none)
   uint32_t* loc_[2] = {nullptr, nullptr};  // local roots w_1024^e, e < 512
   uint32_t* rtab_[2][9] = {};              // [dir][b]: staged stage roots of a b-bit pass (Shoup form)
-  bool use_rtab_ = false;
   uint32_t* coset_lo_ = nullptr;           // g^e / n, e < 2^h
   uint32_t* coset_hi_ = nullptr;           // g^(e 2^h)
   uint32_t* coset_pos_ = nullptr;          // g^f(pos) / n by digit-reversed position

@@ -6,13 +6,16 @@
 #include <sys/random.h>
 
 #include <algorithm>
+#include <array>
 #include <chrono>
 #include <condition_variable>
 #include <deque>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <exception>
 #include <future>
+#include <shared_mutex>
 #include <thread>
 
 #include "hip_check.hpp"
@@ -101,41 +104,86 @@ static int env_int(const char* name, int dflt) {
   return (v && *v) ? std::atoi(v) : dflt;
 }
 
-// MSM parameters for a prover: window bits automatic (ZKP_WINDOW_BITS overrides);
-// table depth = W (one bucket set) unless the tables would not fit in half of the free
-// HBM, then the largest depth that does (ZKP_TABLE_DEPTH overrides).
-static void choose_msm_params(size_t n_w, size_t n_h, MsmParams& pw, MsmParams& ph) {
-  // measured on the Venmo shape (tools/gpu/sweep_c2.sh): the witness MSMs (70 % of the digits
-  // of a 0/1-heavy witness are single entries) prefer one bit less than lg n - 4, the
-  // uniform-scalar H MSM one bit more (fewer windows; the bucket reduction is cheap)
+// MSM tuning options: ONE environment variable read when a prover (or a kernel-level MSM) is built,
+// ZKP_MSM = "key=value[,key=value...]" (empty / unset: automatic everything):
+//   w=<bits>  h=<bits>    window bits of the witness plan / the H plan (8..24)
+//   depth=<rows>          base-table rows T per point (1..W; default W, or the largest depth whose
+//                         tables fit half of the free HBM)
+//   task_w=<n> task_h=<n> entries per bucket-accumulation task of either plan (default 32)
+//   seg=<n>               buckets per bucket-reduction segment (a power of two; default 4)
+//   plan=dense|compact    the plan variant of the kernel-level MSMs (zkp_msm_*; default dense)
+// A malformed value or an unknown key is a ZKP_ERR_INVALID_ARG: a typo never silently tunes nothing.
+struct MsmOptions {
+  int w = 0, h = 0, depth = 0, task_w = 0, task_h = 0, seg = 0;
+  int dense = 1;
+};
+static MsmOptions msm_options() {
+  MsmOptions o;
+  const char* e = std::getenv("ZKP_MSM");
+  if (!e) return o;
+  std::string spec(e);
+  size_t at = 0;
+  while (at < spec.size()) {
+    size_t end = spec.find(',', at);
+    if (end == std::string::npos) end = spec.size();
+    const std::string item = spec.substr(at, end - at);
+    at = end + 1;
+    if (item.empty()) continue;
+    const size_t eq = item.find('=');
+    if (eq == std::string::npos) throw ZkpError(ZKP_ERR_INVALID_ARG, "ZKP_MSM: '" + item + "' is not key=value");
+    const std::string key = item.substr(0, eq), val = item.substr(eq + 1);
+    if (key == "plan") {
+      if (val != "dense" && val != "compact") throw ZkpError(ZKP_ERR_INVALID_ARG, "ZKP_MSM: plan=dense|compact");
+      o.dense = val == "dense" ? 1 : 0;
+      continue;
+    }
+    char* stop = nullptr;
+    const long v = std::strtol(val.c_str(), &stop, 10);
+    if (val.empty() || *stop || v <= 0 || v > (1 << 20))
+      throw ZkpError(ZKP_ERR_INVALID_ARG, "ZKP_MSM: bad value in '" + item + "'");
+    int* dst = key == "w" ? &o.w : key == "h" ? &o.h : key == "depth" ? &o.depth : key == "task_w" ? &o.task_w
+             : key == "task_h" ? &o.task_h : key == "seg" ? &o.seg : nullptr;
+    if (!dst) throw ZkpError(ZKP_ERR_INVALID_ARG, "ZKP_MSM: unknown key '" + key + "'");
+    if (key == "seg" && (v & (v - 1))) throw ZkpError(ZKP_ERR_INVALID_ARG, "ZKP_MSM: seg must be a power of two");
+    *dst = (int)v;
+  }
+  return o;
+}
+
+static MsmParams make_params(size_t n, int c, int depth) {
+  try {
+    return MsmParams::make(n, c, depth);
+  } catch (const std::invalid_argument& x) {
+    throw ZkpError(ZKP_ERR_INVALID_ARG, x.what());
+  }
+}
+
+// MSM parameters for a prover: window bits automatic (ZKP_MSM w= / h= override); table depth = W
+// (one bucket set) unless the tables would not fit in half of the free HBM, then the largest depth
+// that does (ZKP_MSM depth= overrides).
+static void choose_msm_params(size_t n_w, size_t n_h, const MsmOptions& o, MsmParams& pw, MsmParams& ph) {
+  // measured on the Venmo shape (tools/gpu/experiments/sweep_c2.sh): the witness MSMs (70 % of the
+  // digits of a 0/1-heavy witness are single entries) prefer one bit less than lg n - 4, the
+  // uniform-scalar H MSM one bit more (fewer windows; the bucket reduction is cheap), moved off the
+  // widths whose top window collapses into a few buckets (dense_window_bits)
   auto lg = [](size_t n) {
     int l = 0;
     while ((size_t(1) << l) < n) ++l;
     return l;
   };
   auto clampc = [](int c) { return c < 8 ? 8 : (c > 20 ? 20 : c); };
-  const int c = env_int("ZKP_WINDOW_BITS", 0), d = env_int("ZKP_TABLE_DEPTH", 0);
-  const int cw = env_int("ZKP_WINDOW_BITS_W", c ? c : clampc(lg(n_w) - 5));
-  // the H plan's windows: balanced widths (ZKP_H_BALANCED=1: nb1 x c + (W - nb1) x (c - 1) bits, no
-  // narrow top window), else uniform c-bit windows with c moved off the widths whose top window
-  // collapses into a few buckets (dense_window_bits)
-  const bool hbal = env_int("ZKP_H_BALANCED", 0) == 1;
-  const int ch = env_int("ZKP_WINDOW_BITS_H", c ? c : (hbal ? clampc(lg(n_h) - 3) : dense_window_bits(clampc(lg(n_h) - 3), n_h)));
-  const int sw = env_int("ZKP_TASK_W", 0), sh = env_int("ZKP_TASK_H", 0);  // entries per task (tuning)
-  // buckets per reduction segment / subset-sum fan-in (tuning; powers of two)
-  const int sm = env_int("ZKP_SEG_M", 0), sl = env_int("ZKP_SUB_L", 0);
-  auto tasks = [&] {
-    if (sw > 0) pw.S = sw;
-    if (sh > 0) ph.S = sh;
-    for (MsmParams* q : {&pw, &ph}) {
-      if (sm > 0 && (sm & (sm - 1)) == 0 && sm <= (1 << (q->c - 1))) q->M = sm;
-      if (sl > 1) q->L = sl;
-    }
+  const int cw = o.w ? o.w : clampc(lg(n_w) - 5);
+  const int ch = o.h ? o.h : dense_window_bits(clampc(lg(n_h) - 3), n_h);
+  auto tune = [&] {
+    if (o.task_w > 0) pw.S = o.task_w;
+    if (o.task_h > 0) ph.S = o.task_h;
+    for (MsmParams* q : {&pw, &ph})
+      if (o.seg > 0 && o.seg <= (1 << (q->c - 1))) q->M = o.seg;
   };
-  pw = MsmParams::make(n_w, cw, d);
-  ph = MsmParams::make(n_h, ch, d, hbal);
-  tasks();
-  if (d > 0) return;
+  pw = make_params(n_w, cw, o.depth);
+  ph = make_params(n_h, ch, o.depth);
+  tune();
+  if (o.depth > 0) return;
   size_t free_b = 0, total_b = 0;
   HIPX(hipMemGetInfo(&free_b, &total_b));
   const size_t row_w = n_w * (3 * 64 + 128), row_h = n_h * 64;
@@ -143,9 +191,9 @@ static void choose_msm_params(size_t n_w, size_t n_h, MsmParams& pw, MsmParams& 
   int depth = std::max(pw.windows, ph.windows);
   while (depth > 1 && (size_t)std::min(depth, pw.windows) * row_w + (size_t)std::min(depth, ph.windows) * row_h > budget)
     --depth;
-  pw = MsmParams::make(n_w, cw, depth);
-  ph = MsmParams::make(n_h, ch, depth, hbal);
-  tasks();
+  pw = make_params(n_w, cw, depth);
+  ph = make_params(n_h, ch, depth);
+  tune();
 }
 
 // upload `count` zkey points (snarkjs LEM layout) into row 0 of a base table at point
@@ -244,28 +292,8 @@ class DevicePipeline {
     int prio_lo = 0, prio_hi = 0;
     HIPX(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
     HIPX(hipStreamCreateWithPriority(&s0_, hipStreamNonBlocking, prio_hi));
-    // ZKP_RESERVE_CUS = r > 0: the witness-MSM streams s1, s2 run on all CUs but r, so the
-    // critical chain on s0 always finds free CUs: its memory-bound H plan (radix sort)
-    // otherwise gets workgroup slots only as the long accumulation workgroups retire
-    const int reserve = serial_ ? 0 : env_int("ZKP_RESERVE_CUS", 0);
-    hipDeviceProp_t prop;
-    HIPX(hipGetDeviceProperties(&prop, dev_));
-    const int ncu = prop.multiProcessorCount;
-    if (reserve > 0 && reserve < ncu) {
-      std::vector<uint32_t> mask((ncu + 31) / 32, 0);
-      for (int i = 0; i < ncu; ++i)  // r evenly spaced CUs left out
-        if ((int64_t)i * reserve / ncu == (int64_t)(i + 1) * reserve / ncu) mask[i / 32] |= 1u << (i % 32);
-      HIPX(hipExtStreamCreateWithCUMask(&s1_, (uint32_t)mask.size(), mask.data()));
-      HIPX(hipExtStreamCreateWithCUMask(&s2_, (uint32_t)mask.size(), mask.data()));
-      // ... and the H plan (digits + radix sort: memory-bound, and its decoupled look-back
-      // stalls behind any block that shares a CU with the accumulations) runs on just those r
-      for (auto& w : mask) w = ~w;
-      if (ncu % 32) mask.back() &= (1u << (ncu % 32)) - 1;
-      HIPX(hipExtStreamCreateWithCUMask(&s4_, (uint32_t)mask.size(), mask.data()));
-    } else {
-      HIPX(hipStreamCreateWithPriority(&s1_, hipStreamNonBlocking, prio_lo));
-      HIPX(hipStreamCreateWithPriority(&s2_, hipStreamNonBlocking, prio_lo));
-    }
+    HIPX(hipStreamCreateWithPriority(&s1_, hipStreamNonBlocking, prio_lo));
+    HIPX(hipStreamCreateWithPriority(&s2_, hipStreamNonBlocking, prio_lo));
     // s3 runs every MSM's finish (merges + reduction: short latency-bound launches) at high
     // priority, so they slip in between the long accumulations instead of queueing behind them
     HIPX(hipStreamCreateWithPriority(&s3_, hipStreamNonBlocking, prio_hi));
@@ -276,7 +304,7 @@ class DevicePipeline {
     split_range(h.domain_size, part, nparts, hlo_, hhi_);
     const size_t nv = whi_ - wlo_, nd = hhi_ - hlo_;
     MsmParams pw, ph;
-    choose_msm_params(nv, nd, pw, ph);
+    choose_msm_params(nv, nd, msm_options(), pw, ph);
     // base tables: A, B1, C, B2 indexed by witness signal (C's first nPublic+1 bases are
     // infinity, so one witness plan serves all four), H by domain index
     if (share) {
@@ -289,7 +317,7 @@ class DevicePipeline {
       tb1_ = std::make_shared<MsmBases>(Curve::G1, nv, pw.c, pw.depth);
       tc_ = std::make_shared<MsmBases>(Curve::G1, nv, pw.c, pw.depth);
       tb2_ = std::make_shared<MsmBases>(Curve::G2, nv, pw.c, pw.depth);
-      th_ = std::make_shared<MsmBases>(Curve::G1, nd, ph.c, ph.depth, ph.nb1);
+      th_ = std::make_shared<MsmBases>(Curve::G1, nd, ph.c, ph.depth);
       fill_bases(*ta_, z.bf.sec[5].ptr + wlo_ * 64, nv, 0, s0_);
       fill_bases(*tb1_, z.bf.sec[6].ptr + wlo_ * 64, nv, 0, s0_);
       fill_bases(*tb2_, z.bf.sec[7].ptr + wlo_ * 128, nv, 0, s0_);
@@ -314,26 +342,25 @@ class DevicePipeline {
       }
     }
     // witness upload slots: each has its own copy stream, so a proof's
-    // witness H2D runs outside the compute lock and overlaps the proof in flight
+    // witness H2D runs outside the compute lock and overlaps the proof in flight, and its own pinned
+    // staging buffer and copy threads (upload())
     for (int k = 0; k < NUP; ++k) {
       HIPX(hipMalloc(&up_[k], std::max<size_t>((size_t)h.n_vars * 32, 32)));
+      HIPX(hipHostMalloc(&uph_[k], std::max<size_t>((size_t)h.n_vars * 32, 32), hipHostMallocDefault));
       HIPX(hipStreamCreateWithFlags(&sup_[k], hipStreamNonBlocking));
-      HIPX(hipEventCreate(&upev_[k][0]));
-      HIPX(hipEventCreate(&upev_[k][1]));
+      for (auto& t : copiers_[k]) t = std::make_unique<JobThread>();
     }
     for (auto& b : abc_) HIPX(hipMalloc(&b, nd_all * 32));
     HIPX(hipMalloc(&pscal_, nd_all * 32));
     ntt_ = std::make_unique<NttEngine>((int)h.log_domain, s0_);
-    // the witness plan (built on s2) feeds A/B1/C on s2 and B2 on s1; they overlap the
-    // quotient on s0, which then plans and runs the H MSM
-    // the witness plan on the high-priority finish stream s3 (ahead of its G1 finishes), so its sort
-    // passes are not starved by the quotient's NTTs on s0: the witness accumulations start ~5 ms
-    // earlier; proof 26.69 -> 26.58 ms on one box (profiles/wplan_r03.txt; ZKP_WPLAN_HI=0: s2)
-    plan_w_ = std::make_unique<MsmPlan>(nv, pw, env_int("ZKP_WPLAN_HI", 1) == 1 ? s3_ : s2_);
-    plan_h_ = std::make_unique<MsmPlan>(nd, ph, s4_ ? s4_ : s0_);
-    // H scalars are uniform (quotient evaluations): dense digits, so the H plan never blocks
-    // its host thread and the chain quotient -> plan -> H MSM is enqueued in one go
-    plan_h_->set_dense(env_int("ZKP_H_DENSE", 1) != 0);
+    // the witness plan feeds A/B1/C on s2 and B2 on s1; they overlap the quotient on s0, which then
+    // plans and runs the H MSM.  The witness plan runs on the high-priority finish stream s3 (ahead
+    // of its G1 finishes), so its sort passes are not starved by the quotient's NTTs on s0: the
+    // witness accumulations start ~5 ms earlier; proof 26.69 -> 26.58 ms (profiles/wplan_r03.txt)
+    plan_w_ = std::make_unique<MsmPlan>(nv, pw, s3_);
+    plan_h_ = std::make_unique<MsmPlan>(nd, ph, s0_);
+    // H scalars are uniform (quotient evaluations): dense plan (one workgroup per sub-bin)
+    plan_h_->set_dense(true);
     for (auto& g : g1w_) g = std::make_unique<MsmEngine>(Curve::G1, pw, nv, s2_);
     g2_ = std::make_unique<MsmEngine>(Curve::G2, pw, nv, s1_);
     g1h_ = std::make_unique<MsmEngine>(Curve::G1, ph, nd, s0_);
@@ -368,15 +395,14 @@ class DevicePipeline {
     if (hwin_) (void)hipHostFree(hwin_);
     for (auto& e : ev_) (void)hipEventDestroy(e);
     for (int k = 0; k < NUP; ++k) {
-      if (sup_[k]) (void)hipStreamDestroy(sup_[k]);
-      for (auto& e : upev_[k])
-        if (e) (void)hipEventDestroy(e);
+      for (auto& t : copiers_[k]) t.reset();
+      if (sup_[k]) (void)hipStreamSynchronize(sup_[k]), (void)hipStreamDestroy(sup_[k]);
+      if (uph_[k]) (void)hipHostFree(uph_[k]);
     }
     (void)hipStreamDestroy(s0_);
     (void)hipStreamDestroy(s1_);
     (void)hipStreamDestroy(s2_);
     (void)hipStreamDestroy(s3_);
-    if (s4_) (void)hipStreamDestroy(s4_);
   }
 
   struct MsmOut {
@@ -388,10 +414,10 @@ class DevicePipeline {
   using EarlyFn = std::function<void(const MsmOut&)>;
 
   // ---- witness upload slots.  acquire_upload() blocks until one of the NUP slots is free;
-  // upload() copies a witness into it on the slot's stream (pageable H2D, the calling thread
-  // waits for it, the compute streams do not); prove_uploaded() then runs the proof on it
-  // under the compute lock.  Two callers (two zkp_prove threads, or the two batch workers of
-  // a device) thus overlap one proof's upload with the other's compute.
+  // upload() copies a witness into it (the calling thread waits for it, the compute streams do
+  // not); prove_uploaded() then runs the proof on it under the compute lock.  Two callers (two
+  // zkp_prove threads, or the two batch workers of a device) thus overlap one proof's upload with
+  // the other's compute.
   int acquire_upload() {
     std::unique_lock<std::mutex> lk(upmu_);
     upcv_.wait(lk, [&] {
@@ -419,16 +445,41 @@ class DevicePipeline {
     explicit UploadSlot(DevicePipeline* dp) : d(dp), k(dp->acquire_upload()) {}
     ~UploadSlot() { d->release_upload(k); }
   };
-  // H2D of a witness into slot k; returns the copy time (ms, HIP events on the slot stream)
+  // H2D of a witness (pageable host memory, 32 B per signal) into slot k.  A pageable
+  // hipMemcpyAsync bounces through the runtime's small staging buffers on one host thread (205 MB:
+  // 5 ms).  Here NCOPY threads each take a contiguous share and, piece by piece, copy it into the
+  // slot's pinned buffer and enqueue that piece's DMA (pinned -> HBM, the slot's copy stream): the
+  // host copies of the other pieces and the PCIe transfers overlap.  Returns the wall time (ms).
   float upload(int k, const WtnsView& w) {
     HIPX(hipSetDevice(dev_));
-    HIPX(hipEventRecord(upev_[k][0], sup_[k]));
-    HIPX(hipMemcpyAsync(up_[k], w.values, (size_t)hdr_.n_vars * 32, hipMemcpyHostToDevice, sup_[k]));
-    HIPX(hipEventRecord(upev_[k][1], sup_[k]));
-    HIPX(hipStreamSynchronize(sup_[k]));
-    float ms = 0;
-    HIPX(hipEventElapsedTime(&ms, upev_[k][0], upev_[k][1]));
-    return ms;
+    const auto t0 = std::chrono::steady_clock::now();
+    const size_t bytes = (size_t)hdr_.n_vars * 32;
+    const uint8_t* src = w.values;
+    uint8_t* pin = uph_[k];
+    uint8_t* dst = reinterpret_cast<uint8_t*>(up_[k]);
+    hipStream_t st = sup_[k];
+    std::exception_ptr errs[NCOPY];
+    auto part = [&](int t) {
+      try {
+        HIPX(hipSetDevice(dev_));
+        const size_t lo = bytes * t / NCOPY / 64 * 64, hi = t == NCOPY - 1 ? bytes : bytes * (t + 1) / NCOPY / 64 * 64;
+        for (size_t a = lo; a < hi; a += UP_PIECE) {
+          const size_t len = std::min(UP_PIECE, hi - a);
+          std::memcpy(pin + a, src + a, len);
+          HIPX(hipMemcpyAsync(dst + a, pin + a, len, hipMemcpyHostToDevice, st));
+        }
+      } catch (...) {
+        errs[t] = std::current_exception();
+      }
+    };
+    for (int t = 1; t < NCOPY; ++t) copiers_[k][t - 1]->start([&, t] { part(t); });
+    part(0);
+    for (int t = 1; t < NCOPY; ++t) copiers_[k][t - 1]->wait();
+    const hipError_t sync = hipStreamSynchronize(st);  // every enqueued piece has landed (or failed)
+    for (auto& e : errs)
+      if (e) std::rethrow_exception(e);
+    HIPX(sync);
+    return std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
   }
   MsmOut prove_uploaded(int k, float h2d_ms, const EarlyFn& early = {}) {
     std::lock_guard<std::mutex> lk(mu_);
@@ -440,7 +491,7 @@ class DevicePipeline {
     o.ms[0] = h2d_ms;
     return o;
   }
-  // test hook (ZKP_TEST_FAIL_PIPELINE / ZKP_TEST_FAIL_AFTER, read by Prover): this pipeline
+  // test hook (ZKP_TEST_FAIL, read by Prover): this pipeline
   // reports a device failure on its (after+1)-th proof and every later one
   void set_fault_injection(int after) { fail_after_ = after; }
   bool healthy() const { return healthy_.load(); }
@@ -448,19 +499,22 @@ class DevicePipeline {
   int device() const { return dev_; }
 
   // quotient (rows A4..A8) from a device-resident witness; result scalars in pscal_
-  void enqueue_quotient(const uint32_t* d_wit, const std::function<void()>& before_ntt = {}) {
+  void enqueue_quotient(const uint32_t* d_wit) {
     const ZkeyHeader& h = hdr_;
     launch_build_abc(rowptr_[0], col_[0], val_[0], rowptr_[1], col_[1], val_[1], d_wit, h.domain_size, abc_[0],
                      abc_[1], abc_[2], s0_);
     HIPX(hipEventRecord(ev_[2], s0_));
-    if (before_ntt) before_ntt();
     for (auto* b : abc_) ntt_->coset_extend(b);
     launch_join_abc(abc_[0], abc_[1], abc_[2], h.domain_size, pscal_, s0_);
     HIPX(hipEventRecord(ev_[3], s0_));
   }
 
   // keep a witness resident in HBM slot `slot` (benchmarks: timing without PCIe)
-  void stage(int slot, const WtnsView& w) {
+  // Staging slots are written under stage_mu_ held exclusively, and read (slot lookup AND the whole
+  // proof that reads the slot, on this pipeline or a ZKP_INFLIGHT sibling) under stage_mu_ shared:
+  // restaging waits for the proofs that read the old witness.  Lock order: stage_mu_, then mu_.
+  std::unique_lock<std::shared_mutex> lock_stage() { return std::unique_lock<std::shared_mutex>(stage_mu_); }
+  void stage(int slot, const WtnsView& w) {  // caller holds lock_stage()
     std::lock_guard<std::mutex> lk(mu_);
     HIPX(hipSetDevice(dev_));
     if (slot < 0 || slot > 4096) throw ZkpError(ZKP_ERR_INVALID_ARG, "bad staging slot");
@@ -482,11 +536,18 @@ class DevicePipeline {
     g2_->set_instrument(on);
     stats_g1_ = MsmEngine::Stats{};
     stats_g2_ = MsmEngine::Stats{};
+    launches_.clear();
   }
   void stats(MsmEngine::Stats& g1, MsmEngine::Stats& g2) {
     std::lock_guard<std::mutex> lk(mu_);
     g1 = stats_g1_;
     g2 = stats_g2_;
+  }
+  // every instrumented accumulate launch since set_instrument(true): {kind, adds, ms}, kind 0..2 the
+  // witness MSMs A, B1, C (G1), 3 the H MSM (G1), 4 the witness MSM B2 (G2)
+  void launch_records(std::vector<std::array<double, 3>>& out) {
+    std::lock_guard<std::mutex> lk(mu_);
+    out.insert(out.end(), launches_.begin(), launches_.end());
   }
   void msm_params(MsmParams& pw, MsmParams& ph) const {
     pw = plan_w_->params();
@@ -511,6 +572,7 @@ class DevicePipeline {
   // A, 1 B, 2 C) only, each copied whole (domain x 32 bytes, device layout: Montgomery
   // 2^261, 8 packed words) to dst[v], device memory on this device.  Returns when done.
   void quotient_part_staged(int slot, int mask, void* const* dst) {
+    std::shared_lock<std::shared_mutex> sl(stage_mu_);
     std::lock_guard<std::mutex> lk(mu_);
     HIPX(hipSetDevice(dev_));
     const uint32_t* d = slot_ptr(slot);
@@ -529,6 +591,7 @@ class DevicePipeline {
   // stage 2: this slice's partial sums with the H scalars joined (row A8) from abc[0..2] =
   // the coset evaluations of A, B, C at this part's domain slice (device memory, ready)
   MsmOut prove_ext_staged(int slot, const void* const* abc) {
+    std::shared_lock<std::shared_mutex> sl(stage_mu_);
     std::lock_guard<std::mutex> lk(mu_);
     HIPX(hipSetDevice(dev_));
     const uint32_t* d = slot_ptr(slot);
@@ -553,7 +616,12 @@ class DevicePipeline {
     return prove_uploaded(slot.k, ms, early);
   }
 
-  MsmOut prove_staged(int slot, const EarlyFn& early = {}) { return prove_resident(slot_ptr(slot), early); }
+  MsmOut prove_staged(int slot, const EarlyFn& early = {}) {
+    std::shared_lock<std::shared_mutex> sl(stage_mu_);
+    return prove_resident(slot_ptr(slot), early);
+  }
+  // shared hold of this (first) pipeline's staging slots for a proof that reads one of them
+  std::shared_lock<std::shared_mutex> hold_stage() { return std::shared_lock<std::shared_mutex>(stage_mu_); }
 
   // a proof of a witness already resident on this GPU: this pipeline's staging slot, or a
   // ZKP_INFLIGHT sibling's (staged witnesses live in the device's first pipeline)
@@ -585,39 +653,15 @@ class DevicePipeline {
     std::promise<void> planned;
     std::shared_future<void> planned_f = planned.get_future().share();
     bool planned_set = false;
-    // scheduling experiment (ZKP_SCHED=1): the witness MSMs' accumulations wait for the
-    // quotient, so the quotient -> H plan -> H MSM chain gets the GPU first.  Measured: no
-    // gain (33.7 vs 33.5 ms): the proof is bound by the total work, not by the chain, so
-    // the default lets every stream run freely.  Never in the serial profiling mode.
-    // Modes 4 / 5 gate only the G2 MSM (on the quotient / on the H plan too), so its long
-    // accumulation fills the H-plan window instead of competing with the quotient.
-    const bool gate = !serial_ && sched_gate_;
-    std::promise<void> qdone;
-    std::shared_future<void> qdone_f = qdone.get_future().share();
-    bool qdone_set = false;
-    std::promise<void> g1fin;  // the G1 finishes are enqueued on s3
-    std::shared_future<void> g1fin_f = g1fin.get_future().share();
-    bool g1fin_set = false;
-    std::promise<void> hdone;  // H plan enqueued
-    std::shared_future<void> hdone_f = hdone.get_future().share();
-    bool hdone_set = false;
     auto g1_job = [&] {
       try {
         HIPX(hipSetDevice(dev_));
         HIPX(hipStreamWaitEvent(s2_, ev_[1], 0));
         HIPX(hipEventRecord(ev_[9], s2_));
-        if (plan_w_->stream() != s2_) HIPX(hipStreamWaitEvent(plan_w_->stream(), ev_[1], 0));
+        HIPX(hipStreamWaitEvent(plan_w_->stream(), ev_[1], 0));
         plan_w_->build(d_wit + wlo_ * 8, whi_ - wlo_);
         planned.set_value();
         planned_set = true;
-        if (gate && gate_mode_ < 4) {  // accumulate only once the quotient (head of the critical H chain) is done
-          qdone_f.get();
-          HIPX(hipStreamWaitEvent(s2_, ev_[3], 0));
-          if (gate_mode_ >= 2) {  // ... and the H plan
-            hdone_f.get();
-            HIPX(hipStreamWaitEvent(s2_, plan_h_->ready(), 0));
-          }
-        }
         const MsmBases* tabs[3] = {ta_.get(), tb1_.get(), tc_.get()};
         for (int m = 0; m < 3; ++m) {
           g1w_[m]->accumulate(*plan_w_, *tabs[m]);
@@ -630,12 +674,9 @@ class DevicePipeline {
           }
         }
         HIPX(hipEventRecord(ev_[8], s3_));
-        g1fin.set_value();
-        g1fin_set = true;
       } catch (...) {
         err[0] = std::current_exception();
         if (!planned_set) planned.set_exception(std::current_exception());
-        if (!g1fin_set) g1fin.set_exception(std::current_exception());
       }
     };
     auto g2_job = [&] {
@@ -643,34 +684,12 @@ class DevicePipeline {
         planned_f.get();
         HIPX(hipSetDevice(dev_));
         if (serial_) HIPX(hipStreamWaitEvent(s1_, ev_[8], 0));
-        if (gate && gate_mode_ != 3) {  // mode 3: the G2 MSM (longest finish) runs from the start
-          qdone_f.get();
-          HIPX(hipStreamWaitEvent(s1_, ev_[3], 0));
-          if (gate_mode_ == 2 || gate_mode_ == 5) {
-            hdone_f.get();
-            HIPX(hipStreamWaitEvent(s1_, plan_h_->ready(), 0));
-          }
-        }
         HIPX(hipEventRecord(ev_[7], s1_));
-        // finish on s1 too: s3 is in-order, the G1 finishes must not queue behind it.  With
-        // ZKP_G2_FINISH_GATE=1 the finish (latency-bound merge/reduction chains) waits for the H
-        // plan, so it overlaps the long H accumulation instead of the H plan's sort.
-        // =2: the gated finish goes to the high-priority finish stream s3 (after the G1 finishes
-        // are enqueued there), so it is not starved by the high-priority H accumulation.
+        // the finish on s1 too: s3 is in-order, the G1 finishes must not queue behind it (gating the
+        // G2 finish on the H plan, on either stream, measured +0.9 ms: profiles/g2_finish_r03.txt)
         g2_->accumulate(*plan_w_, *tb2_);
-        hipStream_t fst = s1_;
-        if (!serial_ && g2_finish_gate_) {
-          hdone_f.get();
-          if (g2_finish_gate_ == 2) {
-            g1fin_f.get();
-            HIPX(hipEventRecord(ev_[14], s1_));
-            HIPX(hipStreamWaitEvent(s3_, ev_[14], 0));
-            fst = s3_;
-          }
-          HIPX(hipStreamWaitEvent(fst, plan_h_->ready(), 0));
-        }
-        g2_->finish(*plan_w_, wb2, fst);
-        HIPX(hipEventRecord(ev_[6], fst));
+        g2_->finish(*plan_w_, wb2, s1_);
+        HIPX(hipEventRecord(ev_[6], s1_));
       } catch (...) {
         err[1] = std::current_exception();
       }
@@ -682,27 +701,13 @@ class DevicePipeline {
           HIPX(hipEventRecord(ev_[2], s0_));
           launch_join_abc(ext_abc_[0], ext_abc_[1], ext_abc_[2], (uint32_t)(hhi_ - hlo_), pscal_ + hlo_ * 8, s0_);
           HIPX(hipEventRecord(ev_[3], s0_));
-        } else if (!serial_ && ntt_after_wplan_) {
-          // experiment: the NTTs wait for the witness plan, so its sort is not starved by them
-          // and the witness accumulations start beside the NTTs
-          enqueue_quotient(d_wit, [&] {
-            planned_f.get();
-            HIPX(hipStreamWaitEvent(s0_, plan_w_->ready(), 0));
-          });
         } else {
           enqueue_quotient(d_wit);
         }
-        qdone.set_value();
-        qdone_set = true;
-        if (s4_) HIPX(hipStreamWaitEvent(s4_, ev_[3], 0));
         plan_h_->build(pscal_ + hlo_ * 8, hhi_ - hlo_);
-        hdone.set_value();
-        hdone_set = true;
         g1h_->run(*plan_h_, *th_, wh);
       } catch (...) {
         err[2] = std::current_exception();
-        if (!qdone_set) qdone.set_exception(std::current_exception());
-        if (!hdone_set) hdone.set_exception(std::current_exception());
       }
     };
     if (serial_) {
@@ -752,9 +757,9 @@ class DevicePipeline {
     }
     HIPX(hipStreamSynchronize(s0_));
     HIPX(hipStreamSynchronize(s3_));
-    for (auto& g : g1w_) g->collect(stats_g1_);
-    g1h_->collect(stats_g1_);
-    g2_->collect(stats_g2_);
+    for (int m = 0; m < 3; ++m) collect_kind(*g1w_[m], m, stats_g1_);
+    collect_kind(*g1h_, 3, stats_g1_);
+    collect_kind(*g2_, 4, stats_g2_);
     o.h = msm_fold<HFq>(hwin_ + 3 * wina_, ph);
     HIPX(hipEventElapsedTime(&o.ms[0], ev_[0], ev_[1]));  // wtns H2D
     HIPX(hipEventElapsedTime(&o.ms[1], ev_[1], ev_[2]));  // buildABC
@@ -768,24 +773,22 @@ class DevicePipeline {
  private:
   int dev_;
   size_t wlo_ = 0, whi_ = 0, hlo_ = 0, hhi_ = 0;  // witness / domain slice held by this pipeline
-  bool serial_ = std::getenv("ZKP_SERIAL") && std::getenv("ZKP_SERIAL")[0] == '1';  // profiling: no stream overlap
-  int gate_mode_ = env_int("ZKP_SCHED", 0);
-  int g2_finish_gate_ = env_int("ZKP_G2_FINISH_GATE", 0);
-  bool ntt_after_wplan_ = env_int("ZKP_NTT_AFTER_WPLAN", 0) == 1;
-  bool sched_gate_ = gate_mode_ != 0;
+  bool serial_ = env_int("ZKP_SERIAL", 0) == 1;  // profiling: no stream overlap
   ZkeyHeader hdr_;
   hipStream_t s0_ = nullptr, s1_ = nullptr, s2_ = nullptr, s3_ = nullptr;
-  hipStream_t s4_ = nullptr;  // H plan on the reserved CUs (ZKP_RESERVE_CUS > 0), else s0
   hipEvent_t ev_[16];
   JobThread jt_g1_, jt_g2_;  // host threads feeding s2 (witness plan, G1 MSMs) and s1 (G2 MSM)
   std::shared_ptr<MsmBases> ta_, tb1_, tc_, tb2_, th_;  // shared by the pipelines of one device
   uint32_t* rowptr_[2] = {nullptr, nullptr};
   uint32_t* col_[2] = {nullptr, nullptr};
   uint32_t* val_[2] = {nullptr, nullptr};
-  static constexpr int NUP = 2;  // witness upload slots (double buffering)
+  static constexpr int NUP = 2;    // witness upload slots (double buffering)
+  static constexpr int NCOPY = 4;  // host threads per upload (pageable -> pinned copies, DMA enqueues)
+  static constexpr size_t UP_PIECE = size_t(4) << 20;  // bytes per pinned piece / DMA
   uint32_t* up_[NUP] = {nullptr, nullptr};
+  uint8_t* uph_[NUP] = {nullptr, nullptr};  // pinned staging of each slot
   hipStream_t sup_[NUP] = {nullptr, nullptr};
-  hipEvent_t upev_[NUP][2] = {};
+  std::unique_ptr<JobThread> copiers_[NUP][NCOPY - 1];
   std::mutex upmu_;
   std::condition_variable upcv_;
   bool upbusy_[NUP] = {false, false};
@@ -794,7 +797,7 @@ class DevicePipeline {
   void maybe_inject_fault() {
     if (fail_after_ >= 0 && proofs_done_++ >= fail_after_) {
       healthy_.store(false);
-      throw HipError(hipErrorLaunchFailure, "injected device failure (ZKP_TEST_FAIL_PIPELINE)", __FILE__, __LINE__);
+      throw HipError(hipErrorLaunchFailure, "injected device failure (ZKP_TEST_FAIL)", __FILE__, __LINE__);
     }
   }
   uint32_t* abc_[3] = {nullptr, nullptr, nullptr};
@@ -808,8 +811,18 @@ class DevicePipeline {
   uint32_t* dwin_ = nullptr;
   uint32_t* hwin_ = nullptr;
   std::mutex mu_;
+  std::shared_mutex stage_mu_;  // staging slots (see stage())
   std::vector<uint32_t*> slots_;
   MsmEngine::Stats stats_g1_, stats_g2_;
+  std::vector<std::array<double, 3>> launches_;  // {kind, adds, ms} per instrumented launch (capped)
+  void collect_kind(MsmEngine& e, int kind, MsmEngine::Stats& agg) {
+    MsmEngine::Stats s;
+    e.collect(s);
+    agg.accumulate_ms += s.accumulate_ms, agg.launches += s.launches, agg.mixed_adds += s.mixed_adds;
+    agg.tasks += s.tasks;
+    for (const auto& l : s.per_launch)
+      if (launches_.size() < 65536) launches_.push_back({(double)kind, (double)l.adds, (double)l.ms});
+  }
 };
 
 // ------------------------------------------------------------------ Prover
@@ -862,12 +875,16 @@ Prover::Prover(const uint8_t* zkey, size_t len, const std::vector<int>& devices,
     for (int k = 1; k < inflight_; ++k)
       devs_[(size_t)e * inflight_ + k] = std::make_unique<DevicePipeline>(devs[e], z, part, nparts, first);
   }
-  // test hook: pipeline ZKP_TEST_FAIL_PIPELINE reports a device failure after
-  // ZKP_TEST_FAIL_AFTER proofs (exercises the batch re-queue; never set in production)
+  // test hooks (never set in production): verify-before-return default, a corrupted H partial
+  // (exercises verify-before-return), an injected device failure (exercises the batch re-queue)
   verify_.store(env_int("ZKP_VERIFY", 0) == 1);
   corrupt_h_ = env_int("ZKP_TEST_CORRUPT_H", 0) == 1;
-  const int fp = env_int("ZKP_TEST_FAIL_PIPELINE", -1);
-  if (fp >= 0 && fp < (int)devs_.size()) devs_[fp]->set_fault_injection(env_int("ZKP_TEST_FAIL_AFTER", 0));
+  // ZKP_TEST_FAIL="<pipeline>:<after>": that pipeline reports a device failure from its (after+1)-th proof on
+  if (const char* f = std::getenv("ZKP_TEST_FAIL")) {
+    int fp = -1, after = 0;
+    if (std::sscanf(f, "%d:%d", &fp, &after) == 2 && fp >= 0 && fp < (int)devs_.size())
+      devs_[fp]->set_fault_injection(after);
+  }
 }
 
 // next healthy pipeline in round-robin order (a pipeline that hit a HIP error is skipped)
@@ -1229,6 +1246,7 @@ DevicePipeline& Prover::staged_pipeline(int dev_index) const {
 void Prover::stage(int dev, int slot, const uint8_t* wtns, size_t len) {
   DevicePipeline& d = staged_pipeline(dev);
   WtnsView w = check_wtns(hdr_, wtns, len);
+  auto ex = d.lock_stage();  // no staged proof of this device reads a slot or its public signals now
   d.stage(slot, w);
   std::lock_guard<std::mutex> lk(smu_);
   if (staged_pub_.size() < (size_t)ndevices_) staged_pub_.resize(ndevices_);
@@ -1240,6 +1258,7 @@ void Prover::stage(int dev, int slot, const uint8_t* wtns, size_t len) {
 void Prover::prove_staged(int dev, int slot, const uint8_t* r32, const uint8_t* s32, zkp_proof* out) {
   require_full();
   DevicePipeline& base = staged_pipeline(dev);
+  auto staged = base.hold_stage();  // the slot stays valid and unchanged until the proof is done
   const uint32_t* d_wit = base.slot_ptr(slot);
   // concurrent staged callers on one device take its idle ZKP_INFLIGHT pipelines (the staged
   // witnesses live in the first one; the others read them in place); with none idle the call
@@ -1305,6 +1324,15 @@ void Prover::kernel_stats(double* out, int n) const {
   for (int i = 0; i < n && i < 8; ++i) out[i] = v[i];
 }
 
+int Prover::launch_records(double* out, int max_records) const {
+  std::vector<std::array<double, 3>> all;
+  for (auto& d : devs_) d->launch_records(all);
+  const int n = (int)std::min<size_t>(all.size(), (size_t)std::max(0, max_records));
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < 3; ++j) out[3 * i + j] = all[i][j];
+  return (int)all.size();
+}
+
 // ------------------------------------------------------------------ kernel-level helpers
 
 // One device-resident MSM set-up for the kernel-level entry points: base table from
@@ -1323,20 +1351,19 @@ struct MsmRig {
     HIPX(hipSetDevice(device));
     HIPX(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     try {
-      // automatic window bits and plan: the prover's H-MSM choice (dense plan with the hand-written
-      // bucket sort, c = lg n - 3 clamped to [8, 20]); measured on configs[1] (G1 2^20, uniform
-      // scalars, tools/gpu/r2_msm_c.sh): 1.84 ms against 2.06 ms for the compacted rocprim plan at
-      // c = lg n - 4.  ZKP_MSM_C / ZKP_MSM_DENSE=0 override (A/B).
+      // automatic window bits and plan: the prover's H-MSM choice (dense plan, c = lg n - 3 clamped to
+      // [8, 20] and moved off a collapsed top window); measured on configs[1] (G1 2^20, uniform
+      // scalars, tools/gpu/experiments/r2_msm_c.sh): 1.84 ms against 2.06 ms for a compacted plan at
+      // c = lg n - 4.  ZKP_MSM plan=compact selects the witness plan's variant (tests).
       int lg = 0;
       while ((size_t(1) << lg) < n) ++lg;
-      const bool bal = env_int("ZKP_MSM_BALANCED", env_int("ZKP_H_BALANCED", 0)) == 1;  // as the H plan
-      const int c_raw = std::min(20, std::max(8, lg - 3));
-      const int c_auto = env_int("ZKP_MSM_C", bal ? c_raw : dense_window_bits(c_raw, n));
-      prm = MsmParams::make(std::max<size_t>(n, 1), c ? c : c_auto, depth, bal);
-      bases = std::make_unique<MsmBases>(curve, n, prm.c, prm.depth, prm.nb1);
+      const MsmOptions opt = msm_options();
+      const int c_auto = dense_window_bits(std::min(20, std::max(8, lg - 3)), n);
+      prm = make_params(std::max<size_t>(n, 1), c ? c : c_auto, depth);
+      bases = std::make_unique<MsmBases>(curve, n, prm.c, prm.depth);
       fill_bases(*bases, points, n, 0, st);
       plan = std::make_unique<MsmPlan>(std::max<size_t>(n, 1), prm, st);
-      plan->set_dense(env_int("ZKP_MSM_DENSE", 1) != 0);
+      plan->set_dense(opt.dense != 0);
       eng = std::make_unique<MsmEngine>(curve, prm, std::max<size_t>(n, 1), st);
       HIPX(hipMalloc(&ds, std::max<size_t>(n * 32, 32)));
       HIPX(hipMalloc(&dw, eng->window_words() * 4));
@@ -1446,7 +1473,7 @@ float bench_plan(int device, const uint8_t* scalars, size_t n, int c, int dense,
   try {
     HIPX(hipEventCreate(&e0));
     HIPX(hipEventCreate(&e1));
-    const MsmParams prm = MsmParams::make(n, c, 0, env_int("ZKP_MSM_BALANCED", 0) == 1 && dense);
+    const MsmParams prm = make_params(n, c, 0);
     MsmPlan plan(n, prm, st);
     plan.set_dense(dense != 0);
     HIPX(hipMalloc(&d, n * 32));

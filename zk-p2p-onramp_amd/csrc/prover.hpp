@@ -93,6 +93,8 @@ class Prover {
   // per-kernel HIP-event statistics of the bucket-accumulate kernels
   void set_instrument(bool on);
   void kernel_stats(double* out, int n) const;
+  // per-launch records {kind, mixed adds, ms} (zkp_prover_launch_stats); returns the number held
+  int launch_records(double* out, int max_records) const;
   int device_count() const { return ndevices_; }  // entries of the `devices` list
   int pipelines_per_device() const { return inflight_; }
   // point-range split of one proof: this slice's MSM partial sums

@@ -117,11 +117,9 @@ std::vector<uint8_t> gunzip_if_needed(std::vector<uint8_t> in) {
 }
 
 // run f(k) for k < n on up to hardware_concurrency threads; the first exception is rethrown
-// ZKP_IO_THREADS caps the threads (1 = the sequential cold start, for comparison)
 template <class Fn>
 static void parallel_for(size_t n, Fn f) {
   size_t T = std::max<size_t>(1, std::min<size_t>(n, std::thread::hardware_concurrency()));
-  if (const char* e = std::getenv("ZKP_IO_THREADS")) T = std::max<size_t>(1, std::min<size_t>(T, std::atoi(e)));
   std::atomic<size_t> next{0};
   std::exception_ptr err;
   std::mutex mu;

@@ -30,6 +30,15 @@ function readInput(x) {
   return fs.readFileSync(x);
 }
 
+function sampleHash(buf) {
+  const h = crypto.createHash('sha256').update(buf.subarray(0, Math.min(4096, buf.length)));
+  for (let k = 0; k < 32 && buf.length > 4096; ++k) {
+    const at = Math.floor((buf.length - 256) * (k + 1) / 32);
+    h.update(buf.subarray(at, at + 256));
+  }
+  return h.digest('hex');
+}
+
 function proverFor(zkey, devices) {
   if (typeof zkey === 'string') {
     let h = provers.get(zkey);
@@ -41,10 +50,19 @@ function proverFor(zkey, devices) {
   }
   const src = zkey && typeof zkey === 'object' && zkey.type === 'mem' ? zkey.data : zkey;
   const buf = ArrayBuffer.isView(src) ? Buffer.from(src.buffer, src.byteOffset, src.byteLength) : readInput(zkey);
+  // The full SHA-256 of a key buffer is computed once per (ArrayBuffer, offset, length).  Key
+  // buffers are meant to be immutable; a buffer re-filled with another key (a file re-read into
+  // it, a reused fastfile mem object) is caught by a sampled fingerprint (the first 4 KiB and 32
+  // evenly spaced 256-byte windows) checked on every hit: a mismatch re-hashes the whole buffer.
   let seen = ArrayBuffer.isView(src) ? memKeyHash.get(src.buffer) : undefined;
   let hit = seen && seen.find((e) => e.off === src.byteOffset && e.len === src.byteLength);
+  if (hit && hit.sample !== sampleHash(buf)) {
+    seen.splice(seen.indexOf(hit), 1);
+    hit = undefined;
+  }
   if (!hit) {
-    hit = { off: buf.byteOffset, len: buf.byteLength, hash: crypto.createHash('sha256').update(buf).digest('hex') };
+    hit = { off: buf.byteOffset, len: buf.byteLength, hash: crypto.createHash('sha256').update(buf).digest('hex'),
+            sample: sampleHash(buf) };
     if (ArrayBuffer.isView(src)) {
       if (!seen) memKeyHash.set(src.buffer, (seen = []));
       seen.push(hit);

@@ -100,6 +100,8 @@ def load_library(path: str = LIB_PATH):
         lib.zkp_prove_staged.argtypes = [P, ctypes.c_int, ctypes.c_int, u8p, u8p, ctypes.POINTER(_Proof)]
         lib.zkp_prover_instrument.argtypes = [P, ctypes.c_int]
         lib.zkp_prover_kernel_stats.argtypes = [P, ctypes.POINTER(ctypes.c_double), ctypes.c_int]
+        lib.zkp_prover_launch_stats.argtypes = [P, ctypes.POINTER(ctypes.c_double), ctypes.c_int,
+                                                ctypes.POINTER(ctypes.c_int)]
         lib.zkp_bench_msm.argtypes = [ctypes.c_int, ctypes.c_int, u8p, u8p, sz, ctypes.c_int, ctypes.c_int,
                                       ctypes.POINTER(ctypes.c_double), u8p, ctypes.POINTER(ctypes.c_int)]
         lib.zkp_bench_ntt.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
@@ -141,6 +143,7 @@ def load_library(path: str = LIB_PATH):
                      "zkp_prove_batch", "zkp_prove_batch_status", "zkp_prove_files", "zkp_proof_json", "zkp_public_json",
                      "zkp_prover_timings", "zkp_msm_g1", "zkp_msm_g2", "zkp_ntt_fr", "zkp_quotient",
                      "zkp_witness_stage", "zkp_prove_staged", "zkp_prover_instrument", "zkp_prover_kernel_stats",
+                     "zkp_prover_launch_stats",
                      "zkp_bench_msm", "zkp_bench_ntt", "zkp_bench_plan", "zkp_msm", "zkp_prover_msm_config",
                      "zkp_prover_load_part", "zkp_prove_partial", "zkp_proof_calldata",
                      "zkp_prover_load_chunks", "zkp_zkey_read", "zkp_zkey_read_chunks", "zkp_zkey_contribute", "zkp_zkey_new",
@@ -384,6 +387,19 @@ class Prover:
         v = list(out)
         return {"g1": {"accumulate_ms": v[0], "launches": int(v[1]), "mixed_adds": int(v[2]), "tasks": int(v[3])},
                 "g2": {"accumulate_ms": v[4], "launches": int(v[5]), "mixed_adds": int(v[6]), "tasks": int(v[7])}}
+
+    LAUNCH_KINDS = ("A", "B1", "C", "H", "B2")
+
+    def launch_stats(self):
+        """Every instrumented accumulate launch: [{"msm": "A"|"B1"|"C"|"H"|"B2", "adds": n, "ms": t}]."""
+        lib = load_library()
+        n = ctypes.c_int(0)
+        _check(lib.zkp_prover_launch_stats(self._h, None, 0, ctypes.byref(n)))
+        out = (ctypes.c_double * (3 * max(1, n.value)))()
+        _check(lib.zkp_prover_launch_stats(self._h, out, n.value, ctypes.byref(n)))
+        v = list(out)
+        return [{"msm": self.LAUNCH_KINDS[int(v[3 * i])], "adds": int(v[3 * i + 1]), "ms": v[3 * i + 2]}
+                for i in range(n.value)]
 
     def prove_files(self, wtns_path, proof_path, public_path):
         _check(load_library().zkp_prove_files(self._h, os.fsencode(wtns_path), os.fsencode(proof_path),
