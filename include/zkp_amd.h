@@ -231,7 +231,7 @@ zkp_status zkp_msm_g1(int device, const uint8_t* points, const uint8_t* scalars,
 zkp_status zkp_msm_g2(int device, const uint8_t* points, const uint8_t* scalars, size_t n, uint8_t* out128,
                       int* is_inf);
 /* The same MSM with explicit Pippenger parameters (tests / tuning): window_bits c
- * (0 = automatic, else 2..24) and base-table depth T (0 = automatic = all windows in
+ * (0 = automatic, else 8..24) and base-table depth T (0 = automatic = all windows in
  * one bucket set; 1 = no precomputed rows, one bucket group per window). */
 zkp_status zkp_msm(int device, int g2, const uint8_t* points, const uint8_t* scalars, size_t n, int window_bits,
                    int table_depth, uint8_t* out, int* is_inf);

@@ -39,6 +39,16 @@ int zkp_synth_witness(const zkp_synth_circuit* c, uint64_t wseed, uint8_t* out, 
  * zkp_synth_free).  threads: host threads for the QAP evaluation (0 = all cores). */
 int zkp_synth_zkey(const zkp_synth_circuit* c, uint64_t setup_seed, int device, int threads, uint8_t** out,
                    size_t* len);
+/* The same with gamma = delta = 1 when unit_gamma_delta != 0: the key `snarkjs zkey new` writes from a
+ * ptau of the same tau, alpha, beta (zkp_synth_ptau; sections 2..9 then equal zkp_zkey_new's). */
+int zkp_synth_zkey_ex(const zkp_synth_circuit* c, uint64_t setup_seed, int unit_gamma_delta, int device, int threads,
+                      uint8_t** out, size_t* len);
+/* circom .r1cs (v1) of the synthetic circuit (the layout of oracle/binfile.py write_r1cs) */
+int zkp_synth_r1cs(const zkp_synth_circuit* c, uint8_t** out, size_t* len);
+/* A prepared known-tau .ptau (v1, sections 1-7 and the Lagrange sections 12-15 of every level
+ * 0..power; oracle/binfile.py write_ptau) with tau, alpha, beta of setup_seed as zkp_synth_zkey: every
+ * point on the GPU.  INSECURE (the toxic waste is the seed), for setup benchmarks and tests. */
+int zkp_synth_ptau(uint32_t power, uint64_t setup_seed, int device, int threads, uint8_t** out, size_t* len);
 void zkp_synth_free(uint8_t* buf);
 
 /* k_i * G (G1: 64-byte / G2: 128-byte zkey-layout affine points) for n 32-byte LE scalars */

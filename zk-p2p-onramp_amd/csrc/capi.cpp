@@ -492,8 +492,8 @@ zkp_status zkp_msm_g2(int device, const uint8_t* points, const uint8_t* scalars,
 zkp_status zkp_msm(int device, int g2, const uint8_t* points, const uint8_t* scalars, size_t n, int window_bits,
                    int table_depth, uint8_t* out, int* is_inf) {
   if ((n && (!points || !scalars)) || !out || !is_inf) return fail(ZKP_ERR_INVALID_ARG, "null argument");
-  if (window_bits < 0 || window_bits == 1 || window_bits > 24 || table_depth < 0)
-    return fail(ZKP_ERR_INVALID_ARG, "window_bits must be 0 or 2..24, table_depth >= 0");
+  if (window_bits < 0 || (window_bits > 0 && window_bits < 8) || window_bits > 24 || table_depth < 0)
+    return fail(ZKP_ERR_INVALID_ARG, "MSM window bits must be 0 (automatic) or within 8..24, table_depth >= 0");
   return guard([&] {
     zkp::msm_points(device, g2 ? zkp::Curve::G2 : zkp::Curve::G1, points, scalars, n, out, is_inf, window_bits,
                     table_depth);

@@ -11,10 +11,23 @@ namespace zkp {
 
 namespace {
 
-constexpr int TPB = 256;
-constexpr int LOG_TILE = 10;  // elements per workgroup tile (1024, 36 KiB of LDS)
+constexpr int TPB = 256;  // table kernels
+#ifndef ZKP_NTT_LOG_TILE
+#define ZKP_NTT_LOG_TILE 10
+#endif
+#ifndef ZKP_NTT_TPB
+#define ZKP_NTT_TPB 256
+#endif
+#ifndef ZKP_NTT_MAX_BITS
+#define ZKP_NTT_MAX_BITS 8
+#endif
+#ifndef ZKP_NTT_WPE
+#define ZKP_NTT_WPE 0
+#endif
+constexpr int NTT_TPB = ZKP_NTT_TPB;             // threads per pass workgroup (one radix-4 unit per round)
+constexpr int LOG_TILE = ZKP_NTT_LOG_TILE;       // elements per workgroup tile (2^10: 36 KiB of LDS)
 constexpr int LOC_LOG = 10;   // local-root table: w_1024^e, e < 512
-constexpr int MAX_PASS_BITS = 8;
+constexpr int MAX_PASS_BITS = ZKP_NTT_MAX_BITS;
 constexpr int MAX_TW = 1 << (MAX_PASS_BITS - 1);  // stage roots w_(2^b)^j, j < 2^(b-1), b <= 8
 // the stage-root products are Shoup products by constants (field.hpp mul_shoup: 143 mads, no per-column
 // quotient digits): each root's plain limbs and its quotient floor(w 2^261 / r) are staged in LDS
@@ -44,7 +57,7 @@ struct Tile {
 __device__ __forceinline__ void stage_roots(uint32_t* __restrict__ ltw, const uint32_t* __restrict__ rtab) {
   const uint4* s = reinterpret_cast<const uint4*>(rtab);
   uint4* d = reinterpret_cast<uint4*>(ltw);
-  for (int k = threadIdx.x; k < RW * MAX_TW / 4; k += TPB) d[k] = s[k];
+  for (int k = threadIdx.x; k < RW * MAX_TW / 4; k += NTT_TPB) d[k] = s[k];
 }
 
 // rtab in the LDS layout of stage_roots: ltw[l * MAX_TW + j] = limb l of the plain root w_(2^b)^j,
@@ -161,11 +174,11 @@ __device__ __forceinline__ void dft_stages(uint32_t* __restrict__ lds, const uin
   const uint32_t C = 1u << lc;
   int t = 0;
   for (; t + 1 < b; t += 2) {
-    for (int q = threadIdx.x; q < (E >> 2); q += TPB) r4_unit<LE>(lds, ltw, E, b, lc, t, q);
+    for (int q = threadIdx.x; q < (E >> 2); q += NTT_TPB) r4_unit<LE>(lds, ltw, E, b, lc, t, q);
     __syncthreads();
   }
   if (t < b) {  // odd b: the last radix-2 stage (span 1)
-    for (int q = threadIdx.x; q < (E >> 1); q += TPB) {
+    for (int q = threadIdx.x; q < (E >> 1); q += NTT_TPB) {
       const uint32_t col = (uint32_t)q & (C - 1), bq = ((uint32_t)q >> lc) & ((1u << (b - 1)) - 1);
       const uint32_t bl = (uint32_t)q >> (lc + b - 1);
       const int p0 = swz((int)(bl << (b + lc)) + (int)((bq << 1) << lc) + (int)col), p1 = p0 ^ swz((int)C);
@@ -209,8 +222,13 @@ __device__ __forceinline__ int brev_src(const Tile& T, int e) {
 //    (table by digit-reversed position), forward-root DFT on one LDS-resident tile.
 // tw: w_(2^lm)^(col*row) by position in block (null when n2 == 1).  rootsA / rootsB: the stage
 // roots (the k_root_table of this b and direction), B for MODE 2's forward DFT.
+#if ZKP_NTT_WPE
+#define NTT_WPE_ATTR __attribute__((amdgpu_waves_per_eu(ZKP_NTT_WPE)))
+#else
+#define NTT_WPE_ATTR
+#endif
 template <int MODE, int LE>
-__global__ __launch_bounds__(TPB) void k_ntt(uint32_t* __restrict__ data, Tile T, const uint32_t* __restrict__ tw,
+__global__ __launch_bounds__(NTT_TPB) NTT_WPE_ATTR void k_ntt(uint32_t* __restrict__ data, Tile T, const uint32_t* __restrict__ tw,
                                              const uint32_t* __restrict__ rootsA, const uint32_t* __restrict__ rootsB,
                                              const uint32_t* __restrict__ coset) {
   __shared__ uint32_t lds[NL << LOG_TILE];  // SoA: lds[limb * E + element]
@@ -218,12 +236,12 @@ __global__ __launch_bounds__(TPB) void k_ntt(uint32_t* __restrict__ data, Tile T
   const int E = LE ? (1 << LE) : (1 << (T.b + T.lc + T.lbt));  // LE: the tile size known at compile time
   const uint32_t tile = blockIdx.x;
   stage_roots(ltw, rootsA);
-  constexpr int VPT = (1 << LOG_TILE) / TPB;  // elements per thread of a full tile
+  constexpr int VPT = (1 << LOG_TILE) / NTT_TPB;  // elements per thread of a full tile
   if (LE && MODE == 1 && tw) {
     // full tiles: the twiddle products of two elements at a time in lockstep (mul_pair)
 #pragma unroll
     for (int it = 0; it < VPT; it += 2) {
-      const int e0 = (int)threadIdx.x + it * TPB, e1 = e0 + TPB;
+      const int e0 = (int)threadIdx.x + it * NTT_TPB, e1 = e0 + NTT_TPB;
       size_t g0, g1;
       uint32_t pos0, pos1;
       tile_coords(T, tile, e0, g0, pos0);
@@ -238,7 +256,7 @@ __global__ __launch_bounds__(TPB) void k_ntt(uint32_t* __restrict__ data, Tile T
       }
     }
   } else {
-    for (int e = threadIdx.x; e < E; e += TPB) {
+    for (int e = threadIdx.x; e < E; e += NTT_TPB) {
       size_t g;
       uint32_t pos;
       tile_coords(T, tile, e, g, pos);
@@ -259,7 +277,7 @@ __global__ __launch_bounds__(TPB) void k_ntt(uint32_t* __restrict__ data, Tile T
     if (LE) {
 #pragma unroll
       for (int it = 0; it < VPT; it += 2) {
-        const int e0 = (int)threadIdx.x + it * TPB, e1 = e0 + TPB;
+        const int e0 = (int)threadIdx.x + it * NTT_TPB, e1 = e0 + NTT_TPB;
         const int src0 = swz(brev_src(T, e0)), src1 = swz(brev_src(T, e1));
         Fr x0, x1;
 #pragma unroll
@@ -276,7 +294,7 @@ __global__ __launch_bounds__(TPB) void k_ntt(uint32_t* __restrict__ data, Tile T
     } else {
 #pragma unroll
       for (int it = 0; it < VPT; ++it) {
-        const int e = (int)threadIdx.x + it * TPB;
+        const int e = (int)threadIdx.x + it * NTT_TPB;
         if (e < E) {
           const int src = swz(brev_src(T, e));
           Fr x;
@@ -293,7 +311,7 @@ __global__ __launch_bounds__(TPB) void k_ntt(uint32_t* __restrict__ data, Tile T
     stage_roots(ltw, rootsB);  // the forward roots replace the inverse ones (no reader until the next barrier)
 #pragma unroll
     for (int it = 0; it < VPT; ++it) {
-      const int e = (int)threadIdx.x + it * TPB;
+      const int e = (int)threadIdx.x + it * NTT_TPB;
       if (e < E) {
 #pragma unroll
         for (int l = 0; l < NL; ++l) lds[l * E + swz(e)] = v[it].v[l];
@@ -305,7 +323,7 @@ __global__ __launch_bounds__(TPB) void k_ntt(uint32_t* __restrict__ data, Tile T
   if (LE && MODE == 0 && tw) {
 #pragma unroll
     for (int it = 0; it < VPT; it += 2) {
-      const int e0 = (int)threadIdx.x + it * TPB, e1 = e0 + TPB;
+      const int e0 = (int)threadIdx.x + it * NTT_TPB, e1 = e0 + NTT_TPB;
       const int src0 = swz(brev_src(T, e0)), src1 = swz(brev_src(T, e1));
       Fr x0, x1;
 #pragma unroll
@@ -323,7 +341,7 @@ __global__ __launch_bounds__(TPB) void k_ntt(uint32_t* __restrict__ data, Tile T
       store_fe(data + g1 * 8, y1);
     }
   } else {
-    for (int e = threadIdx.x; e < E; e += TPB) {
+    for (int e = threadIdx.x; e < E; e += NTT_TPB) {
       const int src = swz(brev_src(T, e));
       Fr x;
 #pragma unroll
@@ -556,11 +574,11 @@ void NttEngine::launch_pass(uint32_t* data, int mode, int p, bool inv) {
   auto k1 = full ? k_ntt<1, LOG_TILE> : k_ntt<1, 0>;
   auto k2 = full ? k_ntt<2, LOG_TILE> : k_ntt<2, 0>;
   if (mode == 0)
-    hipLaunchKernelGGL(k0, dim3((unsigned)tiles), dim3(TPB), 0, stream_, data, T, tw_pass_[d][p], ra, none, none);
+    hipLaunchKernelGGL(k0, dim3((unsigned)tiles), dim3(NTT_TPB), 0, stream_, data, T, tw_pass_[d][p], ra, none, none);
   else if (mode == 1)
-    hipLaunchKernelGGL(k1, dim3((unsigned)tiles), dim3(TPB), 0, stream_, data, T, tw_pass_[d][p], ra, none, none);
+    hipLaunchKernelGGL(k1, dim3((unsigned)tiles), dim3(NTT_TPB), 0, stream_, data, T, tw_pass_[d][p], ra, none, none);
   else
-    hipLaunchKernelGGL(k2, dim3((unsigned)tiles), dim3(TPB), 0, stream_, data, T, none, rinv, rfwd, coset_pos_);
+    hipLaunchKernelGGL(k2, dim3((unsigned)tiles), dim3(NTT_TPB), 0, stream_, data, T, none, rinv, rfwd, coset_pos_);
 }
 
 void NttEngine::dif_passes(uint32_t* data, bool inv, int first, int last) {

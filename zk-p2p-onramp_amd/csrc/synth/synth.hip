@@ -543,16 +543,22 @@ void zkp_synth_free(uint8_t* buf) { delete[] buf; }
 
 int zkp_synth_zkey(const zkp_synth_circuit* c, uint64_t setup_seed, int device, int threads, uint8_t** out,
                    size_t* len) {
+  return zkp_synth_zkey_ex(c, setup_seed, 0, device, threads, out, len);
+}
+
+int zkp_synth_zkey_ex(const zkp_synth_circuit* c, uint64_t setup_seed, int unit_gamma_delta, int device, int threads,
+                      uint8_t** out, size_t* len) {
   return guarded([&] {
-    // toxic waste: stream 7, five nonzero fr() (oracle/setup.py toxic_from_seed)
+    // toxic waste: stream 7, five nonzero fr() (oracle/setup.py toxic_from_seed); unit_gamma_delta:
+    // gamma = delta = 1, the key `zkey new` writes from a ptau of the same tau, alpha, beta
     Rng rng(setup_seed, 7);
     U256 tox[5];
     for (auto& v : tox) {
       do v = rng.fr();
       while (host::u256_is_zero(v));
     }
-    const HFr tau = fr_of(tox[0]), alpha = fr_of(tox[1]), beta = fr_of(tox[2]), gamma = fr_of(tox[3]),
-              delta = fr_of(tox[4]);
+    const HFr tau = fr_of(tox[0]), alpha = fr_of(tox[1]), beta = fr_of(tox[2]),
+              gamma = unit_gamma_delta ? HFr::one() : fr_of(tox[3]), delta = unit_gamma_delta ? HFr::one() : fr_of(tox[4]);
     const size_t n = c->domain;
     const uint32_t nv = c->n_vars, np = c->n_pub;
     // L_c(tau) = (tau^n - 1)/n * w^c / (tau - w^c)
@@ -670,6 +676,146 @@ int zkp_synth_zkey(const zkp_synth_circuit* c, uint64_t setup_seed, int device, 
       fixed_base<Fq, HFq>(device, sc.data(), sc.size(), buf + off[8], G1);
       fixed_base<Fq, HFq>(device, sh.data(), sh.size(), buf + off[9], G1);
       std::memset(buf + off[10], 0, 68);
+    } catch (...) {
+      delete[] buf;
+      throw;
+    }
+    *out = buf;
+    *len = total;
+  });
+}
+
+int zkp_synth_r1cs(const zkp_synth_circuit* c, uint8_t** out, size_t* len) {
+  return guarded([&] {
+    // circom .r1cs v1 (oracle/binfile.py write_r1cs): 1 header, 2 constraints, 3 wire labels; every
+    // public signal a public input
+    Lc l[3];
+    uint64_t len2 = 0;
+    for (uint32_t k = 0; k < c->n_cons; ++k) {
+      c->constraint(k, l[0], l[1], l[2]);
+      for (auto& x : l) len2 += 4 + 36 * (uint64_t)x.n;
+    }
+    const uint64_t lens[4] = {0, 4 + 32 + 16 + 8 + 4, len2, (uint64_t)c->n_vars * 8};
+    const uint64_t total = 12 + 3 * 12 + lens[1] + lens[2] + lens[3];
+    uint8_t* buf = new uint8_t[total];
+    uint8_t* p = buf;
+    std::memcpy(p, "r1cs", 4);
+    const uint32_t hv[2] = {1, 3};
+    std::memcpy(p + 4, hv, 8);
+    p += 12;
+    for (uint32_t sid = 1; sid <= 3; ++sid) {
+      std::memcpy(p, &sid, 4);
+      put_u64(p + 4, lens[sid]);
+      p += 12;
+      if (sid == 1) {
+        const uint32_t n8 = 32;
+        std::memcpy(p, &n8, 4);
+        put_le(p + 4, host::FR_DESC.mod);
+        const uint32_t w4[4] = {c->n_vars, 0, c->n_pub, c->n_vars - 1 - c->n_pub};
+        std::memcpy(p + 36, w4, 16);
+        put_u64(p + 52, c->n_vars);
+        std::memcpy(p + 60, &c->n_cons, 4);
+        p += lens[1];
+      } else if (sid == 2) {
+        for (uint32_t k = 0; k < c->n_cons; ++k) {
+          c->constraint(k, l[0], l[1], l[2]);
+          for (auto& x : l) {
+            const uint32_t cnt = (uint32_t)x.n;
+            std::memcpy(p, &cnt, 4);
+            p += 4;
+            for (int t = 0; t < x.n; ++t, p += 36) {
+              std::memcpy(p, &x.t[t].sig, 4);
+              put_le(p + 4, x.t[t].coef);
+            }
+          }
+        }
+      } else {
+        for (uint32_t i = 0; i < c->n_vars; ++i, p += 8) put_u64(p, i);
+      }
+    }
+    *out = buf;
+    *len = total;
+  });
+}
+
+int zkp_synth_ptau(uint32_t power, uint64_t setup_seed, int device, int threads, uint8_t** out, size_t* len) {
+  return guarded([&] {
+    // a prepared (phase-2-ready) ptau of known tau, alpha, beta (stream 7 as zkp_synth_zkey), the
+    // layout of oracle/binfile.py write_ptau: 1 header, 2 tauG1 (2^(power+1) - 1), 3 tauG2 (2^power),
+    // 4 alphaTauG1, 5 betaTauG1 (2^power each), 6 betaG2, 7 no contributions, 12..15 the Lagrange
+    // forms (lTauG1, lTauG2, lAlphaTauG1, lBetaTauG1) of every level p = 0..power.  INSECURE tooling.
+    if (power < 1 || power > 27) throw std::runtime_error("ptau power must be within 1..27");
+    Rng rng(setup_seed, 7);
+    U256 tox[3];
+    for (auto& v : tox) {
+      do v = rng.fr();
+      while (host::u256_is_zero(v));
+    }
+    const HFr tau = fr_of(tox[0]), alpha = fr_of(tox[1]), beta = fr_of(tox[2]);
+    const uint64_t N = uint64_t(1) << power, NL = (N << 1) - 1;
+    const uint64_t lens[16] = {0, 4 + 32 + 8, NL * 64, N * 128, N * 64, N * 64, 128, 4, 0, 0, 0, 0,
+                               NL * 64, NL * 128, NL * 64, NL * 64};
+    const int ids[11] = {1, 2, 3, 4, 5, 6, 7, 12, 13, 14, 15};
+    uint64_t off[16] = {}, total = 12;
+    for (int id : ids) {
+      off[id] = total + 12;
+      total += 12 + lens[id];
+    }
+    uint8_t* buf = new uint8_t[total];
+    try {
+      std::memcpy(buf, "ptau", 4);
+      const uint32_t hv[2] = {1, 11};
+      std::memcpy(buf + 4, hv, 8);
+      for (int id : ids) {
+        const uint32_t u = (uint32_t)id;
+        std::memcpy(buf + off[id] - 12, &u, 4);
+        put_u64(buf + off[id] - 8, lens[id]);
+      }
+      const uint32_t n8 = 32;
+      std::memcpy(buf + off[1], &n8, 4);
+      put_le(buf + off[1] + 4, host::FQ_DESC.mod);
+      std::memcpy(buf + off[1] + 36, &power, 4);
+      std::memcpy(buf + off[1] + 40, &power, 4);
+      std::memset(buf + off[7], 0, 4);
+      const auto G1 = g1_gen();
+      const auto G2 = g2_gen();
+      put_g2_raw(buf + off[6], host::jac_to_aff(host::jac_mul(host::jac_from_aff(G2), beta.to_std())));
+      // the points are stored in Montgomery form like the zkey sections (fixed_base writes that)
+      std::vector<U256> sc;
+      auto powers = [&](uint64_t n, const HFr& k) {  // k tau^i, i < n
+        sc.resize(n);
+        parallel_for(n, threads, [&](size_t a, size_t b) {
+          HFr x = k * fr_pow_u64(tau, a);
+          for (size_t i = a; i < b; ++i, x = x * tau) sc[i] = x.to_std();
+        });
+      };
+      powers(NL, HFr::one());
+      fixed_base<Fq, HFq>(device, sc.data(), NL, buf + off[2], G1);
+      powers(N, HFr::one());
+      fixed_base<Fq2, HFq2>(device, sc.data(), N, buf + off[3], G2);
+      powers(N, alpha);
+      fixed_base<Fq, HFq>(device, sc.data(), N, buf + off[4], G1);
+      powers(N, beta);
+      fixed_base<Fq, HFq>(device, sc.data(), N, buf + off[5], G1);
+      // Lagrange forms: level p = 2^p points at 2^p - 1: L^(2^p)_i(tau) = (tau^m - 1)/m * w^i/(tau - w^i)
+      std::vector<U256> sl(NL), sa(NL), sb(NL);
+      for (uint32_t lvl = 0; lvl <= power; ++lvl) {
+        const size_t m = size_t(1) << lvl;
+        std::vector<HFr> L;
+        const HFr mfr = fr_of(U256{{(uint64_t)m, 0, 0, 0}});
+        lagrange_like(tau, HFr::one(), root_w((int)lvl), (fr_pow_u64(tau, m) - HFr::one()) * mfr.inv(), m, L, threads);
+        parallel_for(m, threads, [&](size_t a, size_t b) {
+          for (size_t i = a; i < b; ++i) {
+            sl[m - 1 + i] = L[i].to_std();
+            sa[m - 1 + i] = (alpha * L[i]).to_std();
+            sb[m - 1 + i] = (beta * L[i]).to_std();
+          }
+        });
+      }
+      fixed_base<Fq, HFq>(device, sl.data(), NL, buf + off[12], G1);
+      fixed_base<Fq2, HFq2>(device, sl.data(), NL, buf + off[13], G2);
+      fixed_base<Fq, HFq>(device, sa.data(), NL, buf + off[14], G1);
+      fixed_base<Fq, HFq>(device, sb.data(), NL, buf + off[15], G1);
     } catch (...) {
       delete[] buf;
       throw;

@@ -510,6 +510,14 @@ def read_zkey(path_or_chunks) -> bytes:
         lib.zkp_buffer_free(out)
 
 
+def _in(buf):
+    """(pointer, length, keepalive) of bytes or of a library-owned buffer (synth.ZkeyBuffer: .ptr / .len)."""
+    if hasattr(buf, "ptr") and hasattr(buf, "len"):
+        return ctypes.cast(buf.ptr, ctypes.POINTER(ctypes.c_uint8)), buf.len, buf
+    p, k = _buf(bytes(buf) or b"\0")
+    return p, len(buf), k
+
+
 def zkey_contribute(zkey: bytes, k: int, device: int = 0) -> bytes:
     """Phase-2 contribution math on the GPU: delta -> k*delta (sections 2, 8, 9)."""
     lib = load_library()
@@ -542,11 +550,11 @@ def zkey_beacon(zkey: bytes, beacon: bytes, num_iterations_exp: int, device: int
     """`snarkjs zkey beacon <in> <out> <hex> <e> [-n=name]` (zkp_zkey_beacon_named): delta -> k*delta
     with k the beacon's secret on the GPU, the type-1 contribution record appended to section 10."""
     lib = load_library()
-    zp, zk = _buf(zkey)
+    zp, zlen, zk = _in(zkey)
     bp, bk = _buf(bytes(beacon) or b"\0")
     out = ctypes.POINTER(ctypes.c_uint8)()
     n = ctypes.c_size_t()
-    _check(lib.zkp_zkey_beacon_named(device, zp, len(zkey), bp, len(beacon), num_iterations_exp,
+    _check(lib.zkp_zkey_beacon_named(device, zp, zlen, bp, len(beacon), num_iterations_exp,
                                      name.encode() if name else None, ctypes.byref(out), ctypes.byref(n)))
     try:
         return _copy_out(out, n.value)
@@ -558,7 +566,7 @@ def zkey_contribute_entropy(zkey: bytes, entropy: str, rand64: bytes = None, nam
     """`snarkjs zkey contribute <in> <out> -e=<entropy> [-n=name]` (zkp_zkey_contribute_entropy):
     rand64 = the 64 random bytes mixed with the entropy (None: /dev/urandom; tests pass fixed bytes)."""
     lib = load_library()
-    zp, zk = _buf(zkey)
+    zp, zlen, zk = _in(zkey)
     rp = None
     if rand64 is not None:
         if len(rand64) != 64:
@@ -566,7 +574,7 @@ def zkey_contribute_entropy(zkey: bytes, entropy: str, rand64: bytes = None, nam
         rp, rk = _buf(bytes(rand64))
     out = ctypes.POINTER(ctypes.c_uint8)()
     n = ctypes.c_size_t()
-    _check(lib.zkp_zkey_contribute_entropy(device, zp, len(zkey), rp, entropy.encode(), name.encode() if name else None,
+    _check(lib.zkp_zkey_contribute_entropy(device, zp, zlen, rp, entropy.encode(), name.encode() if name else None,
                                            ctypes.byref(out), ctypes.byref(n)))
     try:
         return _copy_out(out, n.value)
@@ -586,11 +594,11 @@ def zkey_new(r1cs: bytes, ptau: bytes, device: int = 0) -> bytes:
     """`snarkjs zkey new`: the phase-2 starting key of a circom .r1cs from a prepared .ptau,
     point sections built on the GPU (zkp_zkey_new)."""
     lib = load_library()
-    rp, rk = _buf(r1cs)
-    pp, pk = _buf(ptau)
+    rp, rlen, rk = _in(r1cs)
+    pp, plen, pk = _in(ptau)
     out = ctypes.POINTER(ctypes.c_uint8)()
     n = ctypes.c_size_t()
-    _check(lib.zkp_zkey_new(device, rp, len(r1cs), pp, len(ptau), ctypes.byref(out), ctypes.byref(n)))
+    _check(lib.zkp_zkey_new(device, rp, rlen, pp, plen, ctypes.byref(out), ctypes.byref(n)))
     try:
         return _copy_out(out, n.value)
     finally:

@@ -34,6 +34,11 @@ def lib():
         L.zkp_synth_witness.argtypes = [P, ctypes.c_uint64, u8p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)]
         L.zkp_synth_zkey.argtypes = [P, ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.POINTER(u8p),
                                      ctypes.POINTER(ctypes.c_size_t)]
+        L.zkp_synth_zkey_ex.argtypes = [P, ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                        ctypes.POINTER(u8p), ctypes.POINTER(ctypes.c_size_t)]
+        L.zkp_synth_r1cs.argtypes = [P, ctypes.POINTER(u8p), ctypes.POINTER(ctypes.c_size_t)]
+        L.zkp_synth_ptau.argtypes = [ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.POINTER(u8p),
+                                     ctypes.POINTER(ctypes.c_size_t)]
         L.zkp_synth_free.argtypes = [u8p]
         L.zkp_synth_free.restype = None
         L.zkp_synth_points_g1.argtypes = [ctypes.c_int, u8p, ctypes.c_size_t, u8p]
@@ -79,11 +84,30 @@ class Circuit:
                                      ctypes.byref(n)))
         return bytes(buf)
 
-    def zkey(self, setup_seed, device=0, threads=0) -> "ZkeyBuffer":
+    def zkey(self, setup_seed, device=0, threads=0, unit_gamma_delta=False) -> "ZkeyBuffer":
+        """Known-tau zkey; unit_gamma_delta: gamma = delta = 1, the key `zkey new` writes from
+        ptau(power, setup_seed) (sections 2..9 equal zkp_zkey_new's)."""
         p = ctypes.POINTER(ctypes.c_uint8)()
         n = ctypes.c_size_t()
-        _chk(lib().zkp_synth_zkey(self._h, setup_seed, device, threads, ctypes.byref(p), ctypes.byref(n)))
+        _chk(lib().zkp_synth_zkey_ex(self._h, setup_seed, 1 if unit_gamma_delta else 0, device, threads,
+                                     ctypes.byref(p), ctypes.byref(n)))
         return ZkeyBuffer(p, n.value)
+
+    def r1cs(self) -> "ZkeyBuffer":
+        """The circuit as circom .r1cs bytes (library-owned buffer)."""
+        p = ctypes.POINTER(ctypes.c_uint8)()
+        n = ctypes.c_size_t()
+        _chk(lib().zkp_synth_r1cs(self._h, ctypes.byref(p), ctypes.byref(n)))
+        return ZkeyBuffer(p, n.value)
+
+
+def ptau(power, setup_seed, device=0, threads=0) -> "ZkeyBuffer":
+    """A prepared known-tau .ptau of `power` (tau, alpha, beta of setup_seed as Circuit.zkey): every point
+    section computed on the GPU (power 24 for the Venmo shape: ~17 GB).  INSECURE tooling."""
+    p = ctypes.POINTER(ctypes.c_uint8)()
+    n = ctypes.c_size_t()
+    _chk(lib().zkp_synth_ptau(power, setup_seed, device, threads, ctypes.byref(p), ctypes.byref(n)))
+    return ZkeyBuffer(p, n.value)
 
 
 class ZkeyBuffer:
