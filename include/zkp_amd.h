@@ -188,7 +188,8 @@ zkp_status zkp_proof_calldata(const zkp_proof* proof, char* buf, size_t cap, siz
 /* Per-stage device timings (ms) of the last zkp_prove on this handle:
  * [0] wtns H2D, [1] buildABC, [2] NTT/quotient, [3] MSM G1 A,B1,C (own stream, overlaps
  * [1]-[2]), [4] MSM G2 B2 (own stream), [5] host assembly, [6] total wall, [7] MSM G1 H,
- * [8] verify-before-return (host; 0 when off).
+ * [8] verify-before-return (host; 0 when off), [9] the witness transfer's PCIe payload in MB
+ * (compact encoding; 0 for staged proofs).
  * n = capacity of ms (entries beyond n are not written). */
 zkp_status zkp_prover_timings(const zkp_prover* p, float* ms, int n);
 
@@ -271,7 +272,8 @@ zkp_status zkp_prove_partial_ext_staged(zkp_prover* p, int slot, const void* con
 zkp_status zkp_prover_instrument(zkp_prover* p, int on);
 zkp_status zkp_prover_kernel_stats(const zkp_prover* p, double* out, int n);
 /* Every instrumented bucket-accumulate launch since zkp_prover_instrument(p, 1), in order: record i =
- * out[3i .. 3i+2] = {kind, mixed additions, ms (HIP events on the launch's stream)}, kind 0 / 1 / 2 =
+ * out[4i .. 4i+3] = {kind, mixed additions, ms (HIP events on the launch's stream), workgroups of the
+ * launch (to match the dispatch in a kernel trace)}, kind 0 / 1 / 2 =
  * the witness MSMs A / B1 / C (G1), 3 = the H MSM (G1), 4 = the witness MSM B2 (G2).  Writes at most
  * max_records records; *n_records = the number held (up to 65536 per pipeline). */
 zkp_status zkp_prover_launch_stats(const zkp_prover* p, double* out, int max_records, int* n_records);

@@ -1,0 +1,75 @@
+"""The compact witness transfer (prover.hip DevicePipeline::upload + qap.hip k_witness_unpack): the
+host sends each block of 64 signals as its values >= 2^32 (32 B) and the low words of the others,
+the device expands them.  A proof from a host witness must equal oracle/cpu's proof of the same
+witness at the same r, s, whatever the mix of small and large values and wherever they sit in their
+block; the witnesses here span several 64K-signal chunks and end in a ragged block.  Witnesses other
+than the circuit's own do not satisfy it: the proof is still a deterministic function of (key,
+witness, r, s), which is what is compared."""
+import numpy as np
+import pytest
+
+import zkp_amd
+from zkp_amd import synth
+
+pytestmark = pytest.mark.gpu
+R_FIX, S_FIX = 0x1234567, 0x7654321
+NV = 3 * 65536 + 37  # 3 full chunks + a partial one ending in a ragged block
+
+
+@pytest.fixture(scope="module")
+def setup():
+    circ = synth.Circuit(NV, NV + 211, 26, 0x5A4B5032)
+    zk = circ.zkey(0x5A4B5033).bytes()
+    return circ, zk
+
+
+def _values(w: bytes, n: int):
+    off = len(w) - 32 * n
+    return w[:off], np.frombuffer(w, dtype=np.uint32, count=8 * n, offset=off).reshape(n, 8).copy()
+
+
+def _pattern(kind, v, rng):
+    n = v.shape[0]
+    if kind == "all_large":
+        v[:] = rng.integers(0, 1 << 32, size=v.shape, dtype=np.uint64).astype(np.uint32)
+        v[:, 7] &= 0x1FFFFFFF  # < 2^253 < r
+    elif kind == "all_small":
+        v[:] = 0
+        v[:, 0] = rng.integers(0, 1 << 32, size=n, dtype=np.uint64).astype(np.uint32)
+    elif kind == "edges":
+        # per lane: 0, 2^32 - 1 (small), 2^32 (large), only the top word set (large), 1, random
+        k = np.arange(n) % 6
+        v[:] = 0
+        v[k == 1, 0] = 0xFFFFFFFF
+        v[k == 2, 1] = 1
+        v[k == 3, 7] = 0x10000000
+        v[k == 4, 0] = 1
+        r = rng.integers(0, 1 << 32, size=(int((k == 5).sum()), 8), dtype=np.uint64).astype(np.uint32)
+        r[:, 7] &= 0x1FFFFFFF
+        v[k == 5] = r
+        # whole blocks of one kind next to each other
+        v[64 * 5:64 * 6] = 0
+        v[64 * 6:64 * 7, 1] = 0xFFFF
+    v[0] = 0
+    v[0, 0] = 1
+    return v
+
+
+@pytest.mark.parametrize("kind", ["natural", "all_large", "all_small", "edges"])
+def test_host_witness_proof_equals_oracle(setup, kind):
+    from oracle import cpu_oracle
+    circ, zk = setup
+    w = circ.witness(91)
+    if kind != "natural":
+        head, v = _values(w, circ.n_vars)
+        w = head + _pattern(kind, v, np.random.default_rng(5)).tobytes()
+    p = zkp_amd.Prover(zk, devices=[0])
+    try:
+        got, _ = p.prove_raw(w, R_FIX, S_FIX)
+        p.stage(w, slot=1)
+        staged, _ = p.prove_staged_raw(1, R_FIX, S_FIX)
+    finally:
+        p.close()
+    want, _ = cpu_oracle.prove(zk, w, R_FIX, S_FIX, threads=8)
+    assert got == want
+    assert staged == want

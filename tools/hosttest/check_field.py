@@ -135,17 +135,6 @@ def main(n=300):
         checks.append(("x8_lsub8_sqr", lambda v, x=x, d=d: v % P == (d - x) ** 2 * inv_rp_p % P and v < 2 * P))
         checks.append(("x8_mul2", lambda v, x=x, a=a, b=b, d=d: v % P == (d * (d - x) - a * b) * inv_rp_p % P
                        and v < 2 * P))
-    # the G1 Y3 sum of products with BOTH factors unnormalised where allowed (curve.hpp acc_y3 with
-    # acc_xsub_raw): R (s2 - y1 + 2m, normalised) * (q - x3 + 8m, raw limbs) + y * (4m - ppp, raw)
-    y3 = [[rnd.randrange(2 * P) for _ in range(8)] for _ in range(n)]
-    y3 += [[s2, y1, q, a, b, c, yy, pp] for s2 in (0, 2 * P - 1) for y1 in (0, 2 * P - 1) for q in (0, 2 * P - 1)
-           for a in (0, 2 * P - 1) for b in (0, 2 * P - 1) for c in (0, 2 * P - 1) for yy in (0, 2 * P - 1)
-           for pp in (0, 2 * P - 1)]
-    for t in y3:
-        s2, y1, q, a, b, c, yy, pp = t
-        lines.append("y3rawq %s" % " ".join(w8(x) for x in t))
-        want = ((s2 - y1) * (q - (a - b - 2 * c)) - yy * pp) * inv_rp_p % P
-        checks.append(("y3raw", lambda v, want=want: v % P == want and v < 2 * P))
     # lazily reduced G2 accumulator forms (field.hpp sqr_lazy / sub_2x4, curve.hpp acc_y3):
     # inputs at the top of their bounds where 8 words can hold them (6m > 2^256: < 2^256 tested)
     TOP = (1 << 256) - 1

@@ -52,12 +52,6 @@ int main() {
       for (int i = 0; i < NL; ++i) printf("%08x ", q.v[i]);
     }
     else if (o == "sub4r") { Fr a = rdf<FrCfg>(), b = rdf<FrCfg>(); prf(sub4(a, b)); }
-    else if (o == "y3rawq") {  // G1 Y3 = R T + Y D, T = q - x3 + 8m raw, D = 4m - ppp raw (curve.hpp acc_y3)
-      Fq s2 = rdf<FqCfg>(), y1 = rdf<FqCfg>(), q = rdf<FqCfg>(), a = rdf<FqCfg>(), b = rdf<FqCfg>(), c = rdf<FqCfg>();
-      Fq y = rdf<FqCfg>(), ppp = rdf<FqCfg>();
-      const Fq R = lsub(s2, y1), x3 = sub_2x8(a, b, c);
-      prf(mul2(R, rsub16(q, x3), y, rsub(fe_zero<FqCfg>(), ppp)));
-    }
     else if (o == "x8q") {  // lazily reduced accumulator x = a - b - 2c (< 8m) and its consumers
       Fq a = rdf<FqCfg>(), b = rdf<FqCfg>(), c = rdf<FqCfg>(), d = rdf<FqCfg>();
       const Fq x = sub_2x8(a, b, c);

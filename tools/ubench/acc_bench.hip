@@ -6,8 +6,10 @@
 //   ./acc_bench [buckets_log2=19] [entries_per_bucket=208] [reps=5]
 // Variants (template flags):
 //   PF   the next entry's point gathered one addition ahead (double-buffered raw words)
-//   LIMB the table stored as 9 x 29-bit limbs per coordinate (72 B per point, no unpack) with the
-//        negated points in a second table (the sign picks the table: no negation on the device)
+//   LIMB 1: the table stored as 9 x 29-bit limbs per coordinate (72 B per point, no unpack) with the
+//        negated points in a second table (the sign picks the table: no negation on the device);
+//        2: packed 64-B points with the negated table (no unpack saving, no negation)
+//   WPE  waves per SIMD the register allocation targets (1: unbounded, 4: <= 128 VGPRs)
 #include <hip/hip_runtime.h>
 #include <chrono>
 #include <cstdint>
@@ -43,7 +45,7 @@ __device__ __forceinline__ uint64_t mix64(uint64_t x) {
 // random affine "points" (field elements < m, not on the curve: the addition's common path does
 // not care, and every variant must give the same sums), packed (16 words) and as limbs (18 words,
 // plus the negated y in the second table)
-__global__ void k_fill(uint32_t* packed, uint32_t* limbs, uint32_t* limbs_neg, size_t n) {
+__global__ void k_fill(uint32_t* packed, uint32_t* packed_neg, uint32_t* limbs, uint32_t* limbs_neg, size_t n) {
   const size_t i = (size_t)blockIdx.x * TPB + threadIdx.x;
   if (i >= n) return;
   Aff<FA> p;
@@ -60,6 +62,7 @@ __global__ void k_fill(uint32_t* packed, uint32_t* limbs, uint32_t* limbs_neg, s
     limbs[i * 18 + 9 + l] = p.y.v[l];
   }
   const FA ny = sub(fe_zero<FqAccCfg>(), p.y);
+  store_aff(packed_neg, i, Aff<FA>{p.x, ny});
   for (int l = 0; l < NL; ++l) {
     limbs_neg[i * 18 + l] = p.x.v[l];
     limbs_neg[i * 18 + 9 + l] = ny.v[l];
@@ -73,10 +76,10 @@ __global__ void k_vals(uint32_t* vals, size_t n, uint32_t ntab) {
   vals[i] = (uint32_t)(r % ntab) | ((uint32_t)(r >> 40) & 1u) << 31;
 }
 
-template <bool LIMB>
+template <int LIMB>
 __device__ __forceinline__ void load_raw(const uint32_t* __restrict__ tab, const uint32_t* __restrict__ tabn,
                                          uint32_t v, uint32_t (&w)[18]) {
-  if (LIMB) {
+  if (LIMB == 1) {
     const uint32_t* p = ((v >> 31) ? tabn : tab) + (size_t)(v & 0x7fffffffu) * 18;
     const uint2* q = reinterpret_cast<const uint2*>(p);  // 72-B rows: 8-byte aligned
 #pragma unroll
@@ -86,7 +89,7 @@ __device__ __forceinline__ void load_raw(const uint32_t* __restrict__ tab, const
       w[2 * k + 1] = t.y;
     }
   } else {
-    const uint4* q = reinterpret_cast<const uint4*>(tab + (size_t)(v & 0x7fffffffu) * 16);
+    const uint4* q = reinterpret_cast<const uint4*>((LIMB == 2 && (v >> 31) ? tabn : tab) + (size_t)(v & 0x7fffffffu) * 16);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const uint4 t = q[k];
@@ -95,10 +98,10 @@ __device__ __forceinline__ void load_raw(const uint32_t* __restrict__ tab, const
   }
 }
 
-template <bool LIMB>
+template <int LIMB>
 __device__ __forceinline__ Aff<FA> to_aff(const uint32_t (&w)[18]) {
   Aff<FA> p;
-  if (LIMB) {
+  if (LIMB == 1) {
 #pragma unroll
     for (int l = 0; l < NL; ++l) p.x.v[l] = w[l], p.y.v[l] = w[9 + l];
   } else {
@@ -112,7 +115,7 @@ __device__ __forceinline__ Aff<FA> to_aff(const uint32_t (&w)[18]) {
 }
 
 // one task per thread (tasks never straddle a bucket; every bucket of the same length here)
-template <bool PF, bool LIMB, int WPE>
+template <bool PF, int LIMB, int WPE>
 __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(WPE))) void k_acc(const uint32_t* __restrict__ tab, const uint32_t* __restrict__ tabn,
                                              const uint32_t* __restrict__ vals, uint32_t ntask, uint32_t S,
                                              uint32_t per_bucket, uint32_t* __restrict__ out) {
@@ -127,7 +130,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(WPE))) void
     const uint32_t v0 = vals[s0], v1 = vals[s0 + 1];
     load_raw<LIMB>(tab, tabn, v0, w0);
     load_raw<LIMB>(tab, tabn, v1, w1);
-    acc = xyzz_from_aff_pair(to_aff<LIMB>(w0), !LIMB && (v0 >> 31), to_aff<LIMB>(w1), !LIMB && (v1 >> 31));
+    acc = xyzz_from_aff_pair(to_aff<LIMB>(w0), (LIMB == 0) && (v0 >> 31), to_aff<LIMB>(w1), (LIMB == 0) && (v1 >> 31));
     j = s0 + 2;
   }
   if (PF) {
@@ -147,7 +150,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(WPE))) void
         neg = (vn >> 31) != 0;
         vn = j + 2 < s1 ? vals[j + 2] : 0u;
       }
-      xyzz_add_aff(acc, q, !LIMB && ng);
+      xyzz_add_aff(acc, q, (LIMB == 0) && ng);
     }
   } else {
     uint32_t vn = j < s1 ? vals[j] : 0u;
@@ -156,7 +159,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(WPE))) void
       if (j + 1 < s1) vn = vals[j + 1];
       uint32_t w[18];
       load_raw<LIMB>(tab, tabn, v, w);
-      xyzz_add_aff(acc, to_aff<LIMB>(w), !LIMB && (v >> 31));
+      xyzz_add_aff(acc, to_aff<LIMB>(w), (LIMB == 0) && (v >> 31));
     }
   }
   store_xyzz(out, t, acc);
@@ -180,13 +183,14 @@ int main(int argc, char** argv) {
   const size_t ntab = (size_t)13 << 23;  // the H table: 2^23 points x 13 rows
   const size_t entries = (size_t)nb * per;
   const uint32_t tpb = (per + S - 1) / S, ntask = nb * tpb;
-  uint32_t *packed, *limbs, *limbsn, *vals, *start, *end, *off, *out[5];
+  uint32_t *packed, *packedn, *limbs, *limbsn, *vals, *start, *end, *off, *out[5];
   CHK(hipMalloc(&packed, ntab * 64));
+  CHK(hipMalloc(&packedn, ntab * 64));
   CHK(hipMalloc(&limbs, ntab * 72));
   CHK(hipMalloc(&limbsn, ntab * 72));
   CHK(hipMalloc(&vals, entries * 4));
   for (auto& o : out) CHK(hipMalloc(&o, (size_t)ntask * 128));
-  hipLaunchKernelGGL(k_fill, dim3((unsigned)((ntab + TPB - 1) / TPB)), dim3(TPB), 0, 0, packed, limbs, limbsn, ntab);
+  hipLaunchKernelGGL(k_fill, dim3((unsigned)((ntab + TPB - 1) / TPB)), dim3(TPB), 0, 0, packed, packedn, limbs, limbsn, ntab);
   hipLaunchKernelGGL(k_vals, dim3((unsigned)((entries + TPB - 1) / TPB)), dim3(TPB), 0, 0, vals, entries, (uint32_t)ntab);
   {
     std::vector<uint32_t> hs(nb + 1), he(nb + 1), ho(nb + 1);
@@ -227,17 +231,18 @@ int main(int argc, char** argv) {
   }, 0);
 #define VAR(name, PFv, LIMBv, WPEv, slot)                                                                  \
   run(name, [&](int s) {                                                                                   \
-    hipLaunchKernelGGL((k_acc<PFv, LIMBv, WPEv>), grid, dim3(TPB), 0, 0, LIMBv ? limbs : packed,             \
-                       LIMBv ? limbsn : packed, vals, ntask, S, per, out[s]);                              \
+    hipLaunchKernelGGL((k_acc<PFv, LIMBv, WPEv>), grid, dim3(TPB), 0, 0,                                   \
+                       LIMBv == 1 ? limbs : packed, LIMBv == 1 ? limbsn : (LIMBv == 2 ? packedn : packed),    \
+                       vals, ntask, S, per, out[s]);                                                       \
   }, slot)
-  VAR("baseline (packed, select)", false, false, 1, 1);
-  VAR("PF (packed, prefetch)", true, false, 1, 2);
-  VAR("LIMB (72 B limbs, negated table)", false, true, 1, 3);
-  VAR("PF+LIMB", true, true, 1, 4);
-  VAR("baseline, 4 waves", false, false, 4, 1);
-  VAR("PF, 4 waves", true, false, 4, 2);
-  VAR("LIMB, 4 waves", false, true, 4, 3);
-  VAR("PF+LIMB, 4 waves", true, true, 4, 4);
+  VAR("baseline (packed, select)", false, 0, 1, 1);
+  VAR("NEG (packed, negated table)", false, 2, 1, 2);
+  VAR("PF+NEG", true, 2, 1, 3);
+  VAR("LIMB (72 B limbs, negated table)", false, 1, 1, 4);
+  VAR("baseline, 4 waves", false, 0, 4, 1);
+  VAR("NEG, 4 waves", false, 2, 4, 2);
+  VAR("PF, 4 waves", true, 0, 4, 3);
+  VAR("PF+NEG, 4 waves", true, 2, 4, 4);
   CHK(hipDeviceSynchronize());
   std::vector<uint32_t> ref((size_t)ntask * 32), got(ref.size());
   CHK(hipMemcpy(ref.data(), out[0], ref.size() * 4, hipMemcpyDeviceToHost));

@@ -57,10 +57,6 @@ ZDEV Fq2 acc_x3(const Fq2& rr, const Fq2& ppp, const Fq2& q) { return sub_2x4(rr
 template <class C>
 ZDEV Fe<C> acc_xsub(const Fe<C>& a, const Fe<C>& x) { return lsub8(a, x); }  // a - x for an accumulator x
 ZDEV Fq2 acc_xsub(const Fq2& a, const Fq2& x) { return lsub4_lazy(a, x); }
-// Q - X3 as the T factor of Y3 = R T + Y D only: G1 leaves it unnormalised (field.hpp rsub16)
-template <class C>
-ZDEV Fe<C> acc_xsub_t(const Fe<C>& a, const Fe<C>& x) { return rsub16(a, x); }
-ZDEV Fq2 acc_xsub_t(const Fq2& a, const Fq2& x) { return lsub4_lazy(a, x); }
 template <class C>
 ZDEV Fe<C> acc_sub(const Fe<C>& a, const Fe<C>& b) { return lsub(a, b); }  // a - b, both < 2m
 ZDEV Fq2 acc_sub(const Fq2& a, const Fq2& b) { return lsub2_lazy(a, b); }
@@ -222,7 +218,7 @@ ZDEV void xyzz_add_aff(Xyzz<F>& acc, const Aff<F>& q, bool neg = false) {
   F PPP, Q, ZZ3, ZZZ3;
   mul_2(P, PP, acc.x, PP, PPP, Q);
   const F X3 = acc_x3(RR, PPP, Q);
-  const F Y3 = acc_y3(R, acc_xsub_t(Q, X3), acc.y, acc_negd(PPP));  // R (Q - X3) - Y1 PPP
+  const F Y3 = acc_y3(R, acc_xsub(Q, X3), acc.y, acc_negd(PPP));  // R (Q - X3) - Y1 PPP
   mul_2(acc.zz, PP, acc.zzz, PPP, ZZ3, ZZZ3);
   acc.x = X3;
   acc.zz = ZZ3;
@@ -254,7 +250,7 @@ ZDEV Xyzz<F> xyzz_from_aff_pair(const Aff<F>& p, bool np, const Aff<F>& q, bool 
   F PPP = mul(P, PP);
   F Q = mul(p.x, PP);
   acc.x = acc_x3(RR, PPP, Q);
-  acc.y = acc_y3(R, acc_xsub_t(Q, acc.x), py, acc_negd(PPP));  // R (Q - X3) - Y1 PPP
+  acc.y = acc_y3(R, acc_xsub(Q, acc.x), py, acc_negd(PPP));  // R (Q - X3) - Y1 PPP
   acc.zz = PP;
   acc.zzz = PPP;
   return acc;
@@ -285,7 +281,7 @@ ZDEV void xyzz_add(Xyzz<F>& acc, const Xyzz<F>& q) {
   F PPP, Q;
   mul_2(P, PP, U1, PP, PPP, Q);
   F X3 = acc_x3(RR, PPP, Q);
-  F Y3 = acc_y3(R, acc_xsub_t(Q, X3), S1, acc_negd(PPP));  // R (Q - X3) - S1 PPP
+  F Y3 = acc_y3(R, acc_xsub(Q, X3), S1, acc_negd(PPP));  // R (Q - X3) - S1 PPP
   F ZZ, ZZZ;
   mul_2(acc.zz, q.zz, acc.zzz, q.zzz, ZZ, ZZZ);
   mul_2(ZZ, PP, ZZZ, PPP, acc.zz, acc.zzz);

@@ -604,20 +604,6 @@ ZDEV Fe<C> lsub8(const Fe<C>& a, const Fe<C>& b) {
   return s;
 }
 
-// a - b + 16m for a < 2m, b < 8m (normalised), NOT normalised (limbs < 2^30.6, value < 18m): the T
-// factor of the G1 Y3 sum of products mul2(R, T, Y, D) beside a normalised R < 4m, with D = 4m - PPP
-// an rsub() operand of the other product: column sums < 2^63.8 (9 x 2^59.6 + 9 x 2^58.9 + 9 x 2^58),
-// R T + Y D < 80 m^2 (output < 2m).  16m, not 8m: the top limb of 16m in the borrow form exceeds any
-// top limb of b < 8m, so no limb goes negative without a carry pass.  Saves lsub8's carry pass;
-// host-tested at the extremes (op y3rawq).
-template <class C>
-ZDEV Fe<C> rsub16(const Fe<C>& a, const Fe<C>& b) {
-  Fe<C> s;
-#pragma unroll
-  for (int i = 0; i < NL; ++i) s.v[i] = a.v[i] + C::MOD16_BORROW[i] - b.v[i];
-  return s;
-}
-
 // x < 8m (normalised) -> < 2m
 template <class C>
 ZDEV Fe<C> canon8(const Fe<C>& a) { return cond_sub(cond_sub(a, C::MOD4), C::MOD2); }

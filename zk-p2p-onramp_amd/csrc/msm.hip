@@ -444,7 +444,7 @@ void MsmEngine::collect(Stats& s) {
     s.launches += 1;
     s.mixed_adds += adds;
     s.tasks += h_counts_[i];
-    s.per_launch.push_back({ms, adds});
+    s.per_launch.push_back({ms, adds, h_blocks_[i]});
   }
   pending_ = 0;
 }
@@ -466,6 +466,7 @@ void MsmEngine::accumulate(const MsmPlan& plan, const MsmBases& bases) {
     run_accumulate<Fq2>(plan, bases, part_a_, stream_, e0, e1);
   if (slot >= 0) {
     h_total_[slot] = plan.entries();  // every nonzero digit is one mixed addition
+    h_blocks_[slot] = (uint32_t)grid_for(plan.max_tasks_now());
     h_total_dev_[slot] = plan.entries_dev() != nullptr;
     if (h_total_dev_[slot])  // hand-sorted plans: the exact count, not the grid bound n * W
       HIPX(hipMemcpyAsync(&h_counts_[MAX_PENDING + slot], plan.entries_dev(), 4, hipMemcpyDeviceToHost, stream_));

@@ -220,6 +220,7 @@ class MsmEngine {
   struct Launch {
     float ms;       // HIP events on the engine's stream around the launch
     uint32_t adds;  // nonzero digits it accumulated (mixed additions)
+    uint32_t blocks;  // workgroups of the launch (matches a kernel trace's grid size / TPB)
   };
   struct Stats {
     double accumulate_ms = 0;  // summed over launches
@@ -249,7 +250,8 @@ class MsmEngine {
   hipEvent_t ev_[MAX_PENDING][2];
   uint32_t* h_counts_ = nullptr;  // pinned: tasks per pending run, then entries per pending run
   uint32_t h_total_[MAX_PENDING] = {};
-  bool h_total_dev_[MAX_PENDING] = {};  // entries copied from the device (h_counts_[MAX_PENDING + i])
+  bool h_total_dev_[MAX_PENDING] = {};
+  uint32_t h_blocks_[MAX_PENDING] = {};  // entries copied from the device (h_counts_[MAX_PENDING + i])
 };
 
 // merge levels needed for n points with the given params (worst case: one bucket of

@@ -12,22 +12,12 @@ namespace zkp {
 namespace {
 
 constexpr int TPB = 256;  // table kernels
-#ifndef ZKP_NTT_LOG_TILE
-#define ZKP_NTT_LOG_TILE 10
-#endif
-#ifndef ZKP_NTT_TPB
-#define ZKP_NTT_TPB 256
-#endif
-#ifndef ZKP_NTT_MAX_BITS
-#define ZKP_NTT_MAX_BITS 8
-#endif
-#ifndef ZKP_NTT_WPE
-#define ZKP_NTT_WPE 0
-#endif
-constexpr int NTT_TPB = ZKP_NTT_TPB;             // threads per pass workgroup (one radix-4 unit per round)
-constexpr int LOG_TILE = ZKP_NTT_LOG_TILE;       // elements per workgroup tile (2^10: 36 KiB of LDS)
+// tile and pass widths measured against 2^11 / 2^12-element tiles (512 / 1024 threads, 7- and 8-bit
+// passes): the 2^10 tile is fastest at 2^20 and 2^23 (profiles/ntt_tiles_r04.txt)
+constexpr int NTT_TPB = 256;   // threads per pass workgroup (one radix-4 unit per round)
+constexpr int LOG_TILE = 10;   // elements per workgroup tile (2^10: 36 KiB of LDS)
 constexpr int LOC_LOG = 10;   // local-root table: w_1024^e, e < 512
-constexpr int MAX_PASS_BITS = ZKP_NTT_MAX_BITS;
+constexpr int MAX_PASS_BITS = 8;
 constexpr int MAX_TW = 1 << (MAX_PASS_BITS - 1);  // stage roots w_(2^b)^j, j < 2^(b-1), b <= 8
 // the stage-root products are Shoup products by constants (field.hpp mul_shoup: 143 mads, no per-column
 // quotient digits): each root's plain limbs and its quotient floor(w 2^261 / r) are staged in LDS
@@ -222,13 +212,8 @@ __device__ __forceinline__ int brev_src(const Tile& T, int e) {
 //    (table by digit-reversed position), forward-root DFT on one LDS-resident tile.
 // tw: w_(2^lm)^(col*row) by position in block (null when n2 == 1).  rootsA / rootsB: the stage
 // roots (the k_root_table of this b and direction), B for MODE 2's forward DFT.
-#if ZKP_NTT_WPE
-#define NTT_WPE_ATTR __attribute__((amdgpu_waves_per_eu(ZKP_NTT_WPE)))
-#else
-#define NTT_WPE_ATTR
-#endif
 template <int MODE, int LE>
-__global__ __launch_bounds__(NTT_TPB) NTT_WPE_ATTR void k_ntt(uint32_t* __restrict__ data, Tile T, const uint32_t* __restrict__ tw,
+__global__ __launch_bounds__(NTT_TPB) void k_ntt(uint32_t* __restrict__ data, Tile T, const uint32_t* __restrict__ tw,
                                              const uint32_t* __restrict__ rootsA, const uint32_t* __restrict__ rootsB,
                                              const uint32_t* __restrict__ coset) {
   __shared__ uint32_t lds[NL << LOG_TILE];  // SoA: lds[limb * E + element]

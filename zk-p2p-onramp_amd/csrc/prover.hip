@@ -344,11 +344,15 @@ class DevicePipeline {
     // witness upload slots: each has its own copy stream, so a proof's
     // witness H2D runs outside the compute lock and overlaps the proof in flight, and its own pinned
     // staging buffer and copy threads (upload())
-    for (int k = 0; k < NUP; ++k) {
-      HIPX(hipMalloc(&up_[k], std::max<size_t>((size_t)h.n_vars * 32, 32)));
-      HIPX(hipHostMalloc(&uph_[k], std::max<size_t>((size_t)h.n_vars * 32, 32), hipHostMallocDefault));
-      HIPX(hipStreamCreateWithFlags(&sup_[k], hipStreamNonBlocking));
-      for (auto& t : copiers_[k]) t = std::make_unique<JobThread>();
+    {
+      const size_t stage_words = std::max<size_t>(wt_chunks(h.n_vars), 1) * wt_chunk_words();
+      for (int k = 0; k < NUP; ++k) {
+        HIPX(hipMalloc(&up_[k], std::max<size_t>((size_t)h.n_vars * 32, 32)));
+        HIPX(hipMalloc(&upstage_[k], stage_words * 4));
+        HIPX(hipHostMalloc(&uph_[k], stage_words * 4, hipHostMallocDefault));
+        HIPX(hipStreamCreateWithFlags(&sup_[k], hipStreamNonBlocking));
+        for (auto& t : copiers_[k]) t = std::make_unique<JobThread>();
+      }
     }
     for (auto& b : abc_) HIPX(hipMalloc(&b, nd_all * 32));
     HIPX(hipMalloc(&pscal_, nd_all * 32));
@@ -398,6 +402,7 @@ class DevicePipeline {
       for (auto& t : copiers_[k]) t.reset();
       if (sup_[k]) (void)hipStreamSynchronize(sup_[k]), (void)hipStreamDestroy(sup_[k]);
       if (uph_[k]) (void)hipHostFree(uph_[k]);
+      if (upstage_[k]) (void)hipFree(upstage_[k]);
     }
     (void)hipStreamDestroy(s0_);
     (void)hipStreamDestroy(s1_);
@@ -409,6 +414,7 @@ class DevicePipeline {
     Jac<HFq> a, b1, c, h;
     Jac<HFq2> b2;
     float ms[6];
+    float pcie_mb = 0;  // witness transfer payload (prove() from a host witness)
   };
   // called with a, b1, c, b2 folded (h not yet) while the H MSM still runs on the device
   using EarlyFn = std::function<void(const MsmOut&)>;
@@ -445,28 +451,33 @@ class DevicePipeline {
     explicit UploadSlot(DevicePipeline* dp) : d(dp), k(dp->acquire_upload()) {}
     ~UploadSlot() { d->release_upload(k); }
   };
-  // H2D of a witness (pageable host memory, 32 B per signal) into slot k.  A pageable
-  // hipMemcpyAsync bounces through the runtime's small staging buffers on one host thread (205 MB:
-  // 5 ms).  Here NCOPY threads each take a contiguous share and, piece by piece, copy it into the
-  // slot's pinned buffer and enqueue that piece's DMA (pinned -> HBM, the slot's copy stream): the
-  // host copies of the other pieces and the PCIe transfers overlap.  Returns the wall time (ms).
-  float upload(int k, const WtnsView& w) {
+  // H2D of a witness (pageable host memory, 32 B per signal) into slot k.  PCIe is the limit (a
+  // 205 MB witness: ~4.3 ms at ~48 GB/s through pinned memory), so the transfer is COMPACT: NCOPY
+  // host threads encode chunks of 64K signals (qap.hpp WT_*: per block of 64, the values >= 2^32 as
+  // 32 B, the others as their low word, plus a 12-byte block meta) straight into the slot's pinned
+  // buffer and enqueue each chunk's DMA (pinned -> HBM staging, the slot's copy stream) as soon as it
+  // is encoded, so encoding and PCIe overlap; one kernel then expands the chunks into the 32-B
+  // witness layout.  A 0/1-heavy witness moves ~2.5x fewer bytes; an all-uniform one as many plus the
+  // meta.  Returns the wall time (ms).
+  float upload(int k, const WtnsView& w, uint64_t* pcie_bytes = nullptr) {
     HIPX(hipSetDevice(dev_));
     const auto t0 = std::chrono::steady_clock::now();
-    const size_t bytes = (size_t)hdr_.n_vars * 32;
+    const uint32_t n = hdr_.n_vars;
+    const uint32_t nch = wt_chunks(n);
+    const size_t chw = wt_chunk_words();
     const uint8_t* src = w.values;
-    uint8_t* pin = uph_[k];
-    uint8_t* dst = reinterpret_cast<uint8_t*>(up_[k]);
+    uint32_t* pin = reinterpret_cast<uint32_t*>(uph_[k]);
     hipStream_t st = sup_[k];
     std::exception_ptr errs[NCOPY];
+    std::atomic<uint64_t> sent{0};
     auto part = [&](int t) {
       try {
         HIPX(hipSetDevice(dev_));
-        const size_t lo = bytes * t / NCOPY / 64 * 64, hi = t == NCOPY - 1 ? bytes : bytes * (t + 1) / NCOPY / 64 * 64;
-        for (size_t a = lo; a < hi; a += UP_PIECE) {
-          const size_t len = std::min(UP_PIECE, hi - a);
-          std::memcpy(pin + a, src + a, len);
-          HIPX(hipMemcpyAsync(dst + a, pin + a, len, hipMemcpyHostToDevice, st));
+        for (uint32_t c = (uint32_t)t; c < nch; c += NCOPY) {
+          const size_t words = wt_encode_chunk(src, n, c, pin + (size_t)c * chw);
+          HIPX(hipMemcpyAsync(upstage_[k] + (size_t)c * chw, pin + (size_t)c * chw, words * 4, hipMemcpyHostToDevice,
+                              st));
+          sent += words * 4;
         }
       } catch (...) {
         errs[t] = std::current_exception();
@@ -475,10 +486,14 @@ class DevicePipeline {
     for (int t = 1; t < NCOPY; ++t) copiers_[k][t - 1]->start([&, t] { part(t); });
     part(0);
     for (int t = 1; t < NCOPY; ++t) copiers_[k][t - 1]->wait();
-    const hipError_t sync = hipStreamSynchronize(st);  // every enqueued piece has landed (or failed)
     for (auto& e : errs)
-      if (e) std::rethrow_exception(e);
-    HIPX(sync);
+      if (e) {
+        (void)hipStreamSynchronize(st);
+        std::rethrow_exception(e);
+      }
+    launch_witness_unpack(upstage_[k], n, up_[k], st);
+    HIPX(hipStreamSynchronize(st));
+    if (pcie_bytes) *pcie_bytes = sent.load();
     return std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
   }
   MsmOut prove_uploaded(int k, float h2d_ms, const EarlyFn& early = {}) {
@@ -545,7 +560,7 @@ class DevicePipeline {
   }
   // every instrumented accumulate launch since set_instrument(true): {kind, adds, ms}, kind 0..2 the
   // witness MSMs A, B1, C (G1), 3 the H MSM (G1), 4 the witness MSM B2 (G2)
-  void launch_records(std::vector<std::array<double, 3>>& out) {
+  void launch_records(std::vector<std::array<double, 4>>& out) {
     std::lock_guard<std::mutex> lk(mu_);
     out.insert(out.end(), launches_.begin(), launches_.end());
   }
@@ -612,8 +627,11 @@ class DevicePipeline {
 
   MsmOut prove(const WtnsView& w, const EarlyFn& early = {}) {
     UploadSlot slot(this);
-    const float ms = upload(slot.k, w);
-    return prove_uploaded(slot.k, ms, early);
+    uint64_t bytes = 0;
+    const float ms = upload(slot.k, w, &bytes);
+    MsmOut o = prove_uploaded(slot.k, ms, early);
+    o.pcie_mb = (float)(bytes * 1e-6);
+    return o;
   }
 
   MsmOut prove_staged(int slot, const EarlyFn& early = {}) {
@@ -783,10 +801,11 @@ class DevicePipeline {
   uint32_t* col_[2] = {nullptr, nullptr};
   uint32_t* val_[2] = {nullptr, nullptr};
   static constexpr int NUP = 2;    // witness upload slots (double buffering)
-  static constexpr int NCOPY = 4;  // host threads per upload (pageable -> pinned copies, DMA enqueues)
-  static constexpr size_t UP_PIECE = size_t(4) << 20;  // bytes per pinned piece / DMA
-  uint32_t* up_[NUP] = {nullptr, nullptr};
-  uint8_t* uph_[NUP] = {nullptr, nullptr};  // pinned staging of each slot
+  static constexpr int NCOPY = 8;  // host threads per upload (compact encoding into pinned memory, DMA enqueues)
+  uint32_t* up_[NUP] = {nullptr, nullptr};      // the witness slots (32 B per signal)
+  uint32_t* upstage_[NUP] = {nullptr, nullptr};  // compact chunk regions (HBM)
+  uint8_t* uph_[NUP] = {nullptr, nullptr};       // pinned staging of each slot: compact chunk regions
+
   hipStream_t sup_[NUP] = {nullptr, nullptr};
   std::unique_ptr<JobThread> copiers_[NUP][NCOPY - 1];
   std::mutex upmu_;
@@ -814,14 +833,14 @@ class DevicePipeline {
   std::shared_mutex stage_mu_;  // staging slots (see stage())
   std::vector<uint32_t*> slots_;
   MsmEngine::Stats stats_g1_, stats_g2_;
-  std::vector<std::array<double, 3>> launches_;  // {kind, adds, ms} per instrumented launch (capped)
+  std::vector<std::array<double, 4>> launches_;  // {kind, adds, ms, workgroups} per instrumented launch (capped)
   void collect_kind(MsmEngine& e, int kind, MsmEngine::Stats& agg) {
     MsmEngine::Stats s;
     e.collect(s);
     agg.accumulate_ms += s.accumulate_ms, agg.launches += s.launches, agg.mixed_adds += s.mixed_adds;
     agg.tasks += s.tasks;
     for (const auto& l : s.per_launch)
-      if (launches_.size() < 65536) launches_.push_back({(double)kind, (double)l.adds, (double)l.ms});
+      if (launches_.size() < 65536) launches_.push_back({(double)kind, (double)l.adds, (double)l.ms, (double)l.blocks});
   }
 };
 
@@ -1054,6 +1073,7 @@ void Prover::prove_partial(const uint8_t* wtns, size_t len, zkp_partial* out) {
   std::lock_guard<std::mutex> lk(tmu_);
   for (int i = 0; i < 5; ++i) last_ms_[i] = m.ms[i];
   last_ms_[7] = m.ms[5];
+  last_ms_[9] = m.pcie_mb;
 }
 
 void Prover::prove_partial_staged(int slot, zkp_partial* out) {
@@ -1062,6 +1082,7 @@ void Prover::prove_partial_staged(int slot, zkp_partial* out) {
   std::lock_guard<std::mutex> lk(tmu_);
   for (int i = 0; i < 5; ++i) last_ms_[i] = m.ms[i];
   last_ms_[7] = m.ms[5];
+  last_ms_[9] = m.pcie_mb;
 }
 
 void Prover::quotient_part_staged(int slot, int mask, void* const* dst) {
@@ -1075,6 +1096,7 @@ void Prover::prove_partial_ext_staged(int slot, const void* const* abc, zkp_part
   std::lock_guard<std::mutex> lk(tmu_);
   for (int i = 0; i < 5; ++i) last_ms_[i] = m.ms[i];
   last_ms_[7] = m.ms[5];
+  last_ms_[9] = m.pcie_mb;
 }
 
 void proof_combine(const uint8_t* zkey, size_t len, const zkp_partial* parts, int nparts, const uint8_t* wtns,
@@ -1119,6 +1141,7 @@ void Prover::prove(const uint8_t* wtns, size_t len, const uint8_t* r32, const ui
   std::lock_guard<std::mutex> lk(tmu_);
   for (int i = 0; i < 5; ++i) last_ms_[i] = m.ms[i];
   last_ms_[7] = m.ms[5];
+  last_ms_[9] = m.pcie_mb;
   last_ms_[5] = std::chrono::duration<float, std::milli>(t2 - t1).count();
   last_ms_[6] = std::chrono::duration<float, std::milli>(t2 - t0).count();
   last_ms_[8] = vms;
@@ -1233,7 +1256,7 @@ void Prover::quotient(const uint8_t* wtns, size_t len, uint8_t* out) {
 
 void Prover::timings(float* ms, int n) const {
   std::lock_guard<std::mutex> lk(tmu_);
-  for (int i = 0; i < n && i < 9; ++i) ms[i] = last_ms_[i];
+  for (int i = 0; i < n && i < 10; ++i) ms[i] = last_ms_[i];
 }
 
 DevicePipeline& Prover::staged_pipeline(int dev_index) const {
@@ -1294,6 +1317,7 @@ void Prover::prove_staged(int dev, int slot, const uint8_t* r32, const uint8_t* 
   std::lock_guard<std::mutex> lk(tmu_);
   for (int i = 0; i < 5; ++i) last_ms_[i] = m.ms[i];
   last_ms_[7] = m.ms[5];
+  last_ms_[9] = m.pcie_mb;
   last_ms_[5] = std::chrono::duration<float, std::milli>(t2 - t1).count();
   last_ms_[6] = std::chrono::duration<float, std::milli>(t2 - t0).count();
   last_ms_[8] = vms;
@@ -1325,11 +1349,11 @@ void Prover::kernel_stats(double* out, int n) const {
 }
 
 int Prover::launch_records(double* out, int max_records) const {
-  std::vector<std::array<double, 3>> all;
+  std::vector<std::array<double, 4>> all;
   for (auto& d : devs_) d->launch_records(all);
   const int n = (int)std::min<size_t>(all.size(), (size_t)std::max(0, max_records));
   for (int i = 0; i < n; ++i)
-    for (int j = 0; j < 3; ++j) out[3 * i + j] = all[i][j];
+    for (int j = 0; j < 4; ++j) out[4 * i + j] = all[i][j];
   return (int)all.size();
 }
 

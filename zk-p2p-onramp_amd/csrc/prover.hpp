@@ -93,7 +93,7 @@ class Prover {
   // per-kernel HIP-event statistics of the bucket-accumulate kernels
   void set_instrument(bool on);
   void kernel_stats(double* out, int n) const;
-  // per-launch records {kind, mixed adds, ms} (zkp_prover_launch_stats); returns the number held
+  // per-launch records {kind, mixed adds, ms, workgroups} (zkp_prover_launch_stats); returns the number held
   int launch_records(double* out, int max_records) const;
   int device_count() const { return ndevices_; }  // entries of the `devices` list
   int pipelines_per_device() const { return inflight_; }
@@ -130,7 +130,7 @@ class Prover {
   mutable std::mutex smu_;
   std::atomic<unsigned> rr_{0};
   mutable std::mutex tmu_;
-  float last_ms_[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};  // [8]: verify-before-return (host ms)
+  float last_ms_[10] = {};  // [8]: verify-before-return (host ms), [9]: witness transfer MB
   std::atomic<bool> verify_{false};
   bool corrupt_h_ = false;  // test hook ZKP_TEST_CORRUPT_H=1: piH + G1 generator (a silent device error)
   // throws ZkpError(ZKP_ERR_INTERNAL) unless the assembled proof verifies; returns the host ms spent

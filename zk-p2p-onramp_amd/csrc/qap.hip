@@ -82,7 +82,37 @@ __global__ __launch_bounds__(TPB) void k_fq_from_dev(uint32_t* __restrict__ d, s
   store_fe(d + i * 8, from_mont(load_fe<FqCfg>(d + i * 8)));
 }
 
+// one thread per signal: its block's meta, its rank among the block's large / small lanes
+// (wtns_pack.hpp wt_decode_one); the 32-B stores are coalesced, the payload reads mostly so
+__global__ __launch_bounds__(TPB) void k_witness_unpack(const uint32_t* __restrict__ stage, uint32_t n,
+                                                        uint32_t* __restrict__ out) {
+  const uint32_t i = blockIdx.x * TPB + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t g = i / WT_BLOCK, lane = i % WT_BLOCK;
+  const uint32_t* region = stage + (size_t)(g / WT_CHUNK_BLOCKS) * wt_chunk_words();
+  const uint32_t* mb = region + 3 * (size_t)(g % WT_CHUNK_BLOCKS);
+  const uint64_t mask = (uint64_t)mb[0] | ((uint64_t)mb[1] << 32);
+  const uint64_t below = lane ? mask & (~0ull >> (64 - lane)) : 0ull;
+  const uint32_t ns = (uint32_t)__popcll(below), nl = lane - ns, L = WT_BLOCK - (uint32_t)__popcll(mask);
+  const uint32_t* blk = region + WT_META_WORDS + mb[2];
+  uint4* o = reinterpret_cast<uint4*>(out + (size_t)i * 8);
+  if ((mask >> lane) & 1u) {
+    o[0] = make_uint4(blk[8 * L + ns], 0u, 0u, 0u);
+    o[1] = make_uint4(0u, 0u, 0u, 0u);
+  } else {
+    const uint4* q = reinterpret_cast<const uint4*>(blk + 8 * nl);  // block offsets are multiples of 4 words
+    o[0] = q[0];
+    o[1] = q[1];
+  }
+}
+
 }  // namespace
+
+void launch_witness_unpack(const uint32_t* stage, uint32_t n, uint32_t* out, hipStream_t st) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_witness_unpack, dim3(grid_for(n)), dim3(TPB), 0, st, stage, n, out);
+  HIPX(hipGetLastError());
+}
 
 void launch_convert_fq_zkey(uint32_t* data, size_t nelems, hipStream_t st) {
   if (!nelems) return;

@@ -3,6 +3,7 @@
 // Montgomery form, as 8-word MSM scalars).  snarkjs groth16_prove rows A1, A4,
 // A8.
 #pragma once
+#include "wtns_pack.hpp"
 #include <hip/hip_runtime.h>
 #include <cstddef>
 #include <cstdint>
@@ -22,6 +23,9 @@ void launch_build_abc(const uint32_t* rowptr_a, const uint32_t* col_a, const uin
 // p[j] = standard-form canonical (a[j]*b[j] - c[j]) as 8 LE words
 void launch_join_abc(const uint32_t* a, const uint32_t* b, const uint32_t* c, uint32_t n, uint32_t* p,
                      hipStream_t st);
+// Compact witness transfer (wtns_pack.hpp): expands the chunk regions at stage into n x 8-word
+// values at out.
+void launch_witness_unpack(const uint32_t* stage, uint32_t n, uint32_t* out, hipStream_t st);
 // Fr device layout <-> standard 8-word values (tests)
 void launch_fr_to_dev(uint32_t* data, size_t n, hipStream_t st);
 void launch_fr_from_dev(uint32_t* data, size_t n, hipStream_t st);

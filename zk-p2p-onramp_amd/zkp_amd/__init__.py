@@ -320,10 +320,10 @@ class Prover:
 
     def timings(self):
         lib = load_library()
-        ms = (ctypes.c_float * 9)()
-        _check(lib.zkp_prover_timings(self._h, ms, 9))
+        ms = (ctypes.c_float * 10)()
+        _check(lib.zkp_prover_timings(self._h, ms, 10))
         keys = ["wtns_h2d", "build_abc", "ntt_quotient", "msm_g1_abc", "msm_g2", "host_assembly", "total_wall",
-                "msm_g1_h", "verify"]
+                "msm_g1_h", "verify", "wtns_pcie_mb"]
         return dict(zip(keys, list(ms)))
 
     def set_verify(self, on: bool = True):
@@ -391,15 +391,16 @@ class Prover:
     LAUNCH_KINDS = ("A", "B1", "C", "H", "B2")
 
     def launch_stats(self):
-        """Every instrumented accumulate launch: [{"msm": "A"|"B1"|"C"|"H"|"B2", "adds": n, "ms": t}]."""
+        """Every instrumented accumulate launch: [{"msm": "A"|"B1"|"C"|"H"|"B2", "adds": n, "ms": t,
+        "blocks": workgroups}]."""
         lib = load_library()
         n = ctypes.c_int(0)
         _check(lib.zkp_prover_launch_stats(self._h, None, 0, ctypes.byref(n)))
-        out = (ctypes.c_double * (3 * max(1, n.value)))()
+        out = (ctypes.c_double * (4 * max(1, n.value)))()
         _check(lib.zkp_prover_launch_stats(self._h, out, n.value, ctypes.byref(n)))
         v = list(out)
-        return [{"msm": self.LAUNCH_KINDS[int(v[3 * i])], "adds": int(v[3 * i + 1]), "ms": v[3 * i + 2]}
-                for i in range(n.value)]
+        return [{"msm": self.LAUNCH_KINDS[int(v[4 * i])], "adds": int(v[4 * i + 1]), "ms": v[4 * i + 2],
+                 "blocks": int(v[4 * i + 3])} for i in range(n.value)]
 
     def prove_files(self, wtns_path, proof_path, public_path):
         _check(load_library().zkp_prove_files(self._h, os.fsencode(wtns_path), os.fsencode(proof_path),
