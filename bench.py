@@ -659,8 +659,8 @@ def main():
         "witness_upload": {"ms": round(upload_ms, 3), "witness_bytes": wit_bytes,
                            "pcie_bytes": int(max(up_mb) * 1e6),
                            "witness_GBps": round(wit_bytes / (upload_ms * 1e-3) / 1e9, 1) if upload_ms > 0 else None,
-                           "host_encode_threads": 8,
-                           "note": "compact transfer: 8 host threads encode 64K-signal chunks (values < 2^32 as one "
+                           "host_encode_threads": 16,
+                           "note": "compact transfer: 16 host threads encode 64K-signal chunks (values < 2^32 as one "
                                    "word) into pinned memory, each chunk's DMA overlapping the next chunk's encoding, "
                                    "one kernel expands them in HBM; ms = pageable witness -> 32-B layout in HBM"},
         "higher_is_better": True,

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Witness-plan window bits under different witness mixes: for each
+"""Witness-plan (or H-plan, --which h) window bits under different witness mixes: for each
 bool_pct (percent of bit-valued defining steps of the synthetic Venmo-shaped circuit) build
 the circuit, two witnesses and its known-tau key once, then for every witness-plan width c
 (ZKP_MSM "w=<c>": the base tables depend on c, so one prover per c) time staged proofs.
@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--cs", default="17,18,19,20")
     ap.add_argument("--steps", type=int, default=8)
     ap.add_argument("--reps", type=int, default=2, help="passes over the widths (alternating order)")
+    ap.add_argument("--which", default="w", choices=["w", "h"], help="the witness plan (w) or the H plan (h)")
     args = ap.parse_args()
     for bp in [int(x) for x in args.bools.split(",")]:
         t0 = time.time()
@@ -37,7 +38,7 @@ def main():
         ref = None
         cs = [int(x) for x in args.cs.split(",")]
         for rep, c in [(r, c) for r in range(args.reps) for c in (cs if r % 2 == 0 else cs[::-1])]:
-            os.environ["ZKP_MSM"] = "w=%d" % c
+            os.environ["ZKP_MSM"] = "%s=%d" % (args.which, c)
             p = zkp_amd.Prover(zk, devices=[0])
             for i, w in enumerate(wit):
                 p.stage(w, slot=i)
@@ -48,8 +49,8 @@ def main():
             res = [p.prove_staged_raw(i % 2, R_FIX, S_FIX) for i in range(args.steps)]
             el = time.perf_counter() - t1
             ok = first == ref and all(r == ref[i % 2] for i, r in enumerate(res))
-            print(json.dumps({"bool_pct": bp, "w": c, "rep": rep, "ms_per_proof": round(el / args.steps * 1e3, 3),
-                              "steps": args.steps, "msm": p.msm_config()["witness"], "proofs_equal": ok}), flush=True)
+            print(json.dumps({"bool_pct": bp, args.which: c, "rep": rep, "ms_per_proof": round(el / args.steps * 1e3, 3),
+                              "steps": args.steps, "msm": p.msm_config()["witness" if args.which == "w" else "h"], "proofs_equal": ok}), flush=True)
             p.close()
         os.environ.pop("ZKP_MSM", None)
         del zk

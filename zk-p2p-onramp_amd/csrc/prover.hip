@@ -801,7 +801,7 @@ class DevicePipeline {
   uint32_t* col_[2] = {nullptr, nullptr};
   uint32_t* val_[2] = {nullptr, nullptr};
   static constexpr int NUP = 2;    // witness upload slots (double buffering)
-  static constexpr int NCOPY = 8;  // host threads per upload (compact encoding into pinned memory, DMA enqueues)
+  static constexpr int NCOPY = 16;  // host threads per upload (compact encoding into pinned memory, DMA enqueues)
   uint32_t* up_[NUP] = {nullptr, nullptr};      // the witness slots (32 B per signal)
   uint32_t* upstage_[NUP] = {nullptr, nullptr};  // compact chunk regions (HBM)
   uint8_t* uph_[NUP] = {nullptr, nullptr};       // pinned staging of each slot: compact chunk regions
