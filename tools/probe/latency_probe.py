@@ -1,0 +1,56 @@
+#!/usr/bin/env python3
+"""Where the host-witness latency goes beyond upload + staged proof: staged proofs back to back vs
+after an idle gap (GPU clock/power state), and host-witness proofs with their stage timings.
+usage: latency_probe.py  -> JSON lines"""
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "zk-p2p-onramp_amd"))
+import zkp_amd  # noqa: E402
+from zkp_amd import synth  # noqa: E402
+
+R_FIX, S_FIX = 0x1234567, 0x7654321
+
+
+def main():
+    circ = synth.Circuit.venmo(0x5A4B5032)
+    wit = circ.witness(7001)
+    zk = circ.zkey(0x5A4B5033, device=0)
+    p = zkp_amd.Prover(zk, devices=[0])
+    p.stage(wit, slot=0)
+    for _ in range(3):
+        p.prove_staged_raw(0, R_FIX, S_FIX)
+
+    def staged(gap_s, n=8):
+        ts = []
+        for _ in range(n):
+            if gap_s:
+                time.sleep(gap_s)
+            t0 = time.perf_counter()
+            p.prove_staged_raw(0, R_FIX, S_FIX)
+            ts.append((time.perf_counter() - t0) * 1e3)
+        return round(statistics.median(ts), 3), round(min(ts), 3)
+    for gap in (0, 0.003, 0.05):
+        med, mn = staged(gap)
+        print(json.dumps({"staged_gap_ms": gap * 1e3, "median_ms": med, "min_ms": mn}), flush=True)
+    rows = []
+    for _ in range(7):
+        t0 = time.perf_counter()
+        p.prove_raw(wit, R_FIX, S_FIX)
+        el = (time.perf_counter() - t0) * 1e3
+        tm = p.timings()
+        rows.append((el, tm["wtns_h2d"], tm["total_wall"]))
+    rows.sort()
+    el, up, wall = rows[len(rows) // 2]
+    print(json.dumps({"host_witness_median_ms": round(el, 3), "upload_ms": round(up, 3), "total_wall_ms": round(wall, 3),
+                      "outside_total_wall_ms": round(el - wall, 3)}), flush=True)
+    p.close()
+
+
+if __name__ == "__main__":
+    main()

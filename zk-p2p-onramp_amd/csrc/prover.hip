@@ -470,10 +470,11 @@ class DevicePipeline {
     hipStream_t st = sup_[k];
     std::exception_ptr errs[NCOPY];
     std::atomic<uint64_t> sent{0};
+    constexpr int T = NCOPY;
     auto part = [&](int t) {
       try {
         HIPX(hipSetDevice(dev_));
-        for (uint32_t c = (uint32_t)t; c < nch; c += NCOPY) {
+        for (uint32_t c = (uint32_t)t; c < nch; c += (uint32_t)T) {
           const size_t words = wt_encode_chunk(src, n, c, pin + (size_t)c * chw);
           HIPX(hipMemcpyAsync(upstage_[k] + (size_t)c * chw, pin + (size_t)c * chw, words * 4, hipMemcpyHostToDevice,
                               st));
@@ -483,15 +484,20 @@ class DevicePipeline {
         errs[t] = std::current_exception();
       }
     };
-    for (int t = 1; t < NCOPY; ++t) copiers_[k][t - 1]->start([&, t] { part(t); });
+    for (int t = 1; t < T; ++t) copiers_[k][t - 1]->start([&, t] { part(t); });
     part(0);
-    for (int t = 1; t < NCOPY; ++t) copiers_[k][t - 1]->wait();
+    for (int t = 1; t < T; ++t) copiers_[k][t - 1]->wait();
     for (auto& e : errs)
       if (e) {
         (void)hipStreamSynchronize(st);
         std::rethrow_exception(e);
       }
-    launch_witness_unpack(upstage_[k], n, up_[k], st);
+    // one expansion after every chunk's DMA has completed: kernels enqueued by the encode threads
+    // themselves, each behind its own chunk's DMA on the shared stream, read stale chunk data (a
+    // 4-chunk all-large witness, tests/test_gpu_witness_transfer.py), so the stream order of DMAs
+    // enqueued from several host threads is not relied on
+    HIPX(hipStreamSynchronize(st));
+    launch_witness_unpack(upstage_[k], 0, n, up_[k], st);
     HIPX(hipStreamSynchronize(st));
     if (pcie_bytes) *pcie_bytes = sent.load();
     return std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();

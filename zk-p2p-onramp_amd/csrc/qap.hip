@@ -84,9 +84,9 @@ __global__ __launch_bounds__(TPB) void k_fq_from_dev(uint32_t* __restrict__ d, s
 
 // one thread per signal: its block's meta, its rank among the block's large / small lanes
 // (wtns_pack.hpp wt_decode_one); the 32-B stores are coalesced, the payload reads mostly so
-__global__ __launch_bounds__(TPB) void k_witness_unpack(const uint32_t* __restrict__ stage, uint32_t n,
+__global__ __launch_bounds__(TPB) void k_witness_unpack(const uint32_t* __restrict__ stage, uint32_t i0, uint32_t n,
                                                         uint32_t* __restrict__ out) {
-  const uint32_t i = blockIdx.x * TPB + threadIdx.x;
+  const uint32_t i = i0 + blockIdx.x * TPB + threadIdx.x;
   if (i >= n) return;
   const uint32_t g = i / WT_BLOCK, lane = i % WT_BLOCK;
   const uint32_t* region = stage + (size_t)(g / WT_CHUNK_BLOCKS) * wt_chunk_words();
@@ -108,9 +108,9 @@ __global__ __launch_bounds__(TPB) void k_witness_unpack(const uint32_t* __restri
 
 }  // namespace
 
-void launch_witness_unpack(const uint32_t* stage, uint32_t n, uint32_t* out, hipStream_t st) {
-  if (!n) return;
-  hipLaunchKernelGGL(k_witness_unpack, dim3(grid_for(n)), dim3(TPB), 0, st, stage, n, out);
+void launch_witness_unpack(const uint32_t* stage, uint32_t i0, uint32_t i1, uint32_t* out, hipStream_t st) {
+  if (i1 <= i0) return;
+  hipLaunchKernelGGL(k_witness_unpack, dim3(grid_for(i1 - i0)), dim3(TPB), 0, st, stage, i0, i1, out);
   HIPX(hipGetLastError());
 }
 

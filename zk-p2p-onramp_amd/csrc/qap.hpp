@@ -23,9 +23,9 @@ void launch_build_abc(const uint32_t* rowptr_a, const uint32_t* col_a, const uin
 // p[j] = standard-form canonical (a[j]*b[j] - c[j]) as 8 LE words
 void launch_join_abc(const uint32_t* a, const uint32_t* b, const uint32_t* c, uint32_t n, uint32_t* p,
                      hipStream_t st);
-// Compact witness transfer (wtns_pack.hpp): expands the chunk regions at stage into n x 8-word
-// values at out.
-void launch_witness_unpack(const uint32_t* stage, uint32_t n, uint32_t* out, hipStream_t st);
+// Compact witness transfer (wtns_pack.hpp): expands signals [i0, i1) from the chunk regions at stage
+// into 8-word values at out (signal i at out + 8 i).
+void launch_witness_unpack(const uint32_t* stage, uint32_t i0, uint32_t i1, uint32_t* out, hipStream_t st);
 // Fr device layout <-> standard 8-word values (tests)
 void launch_fr_to_dev(uint32_t* data, size_t n, hipStream_t st);
 void launch_fr_from_dev(uint32_t* data, size_t n, hipStream_t st);
