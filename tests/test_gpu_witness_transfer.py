@@ -55,21 +55,45 @@ def _pattern(kind, v, rng):
     return v
 
 
-@pytest.mark.parametrize("kind", ["natural", "all_large", "all_small", "edges"])
-def test_host_witness_proof_equals_oracle(setup, kind):
+_WANT = {}
+
+
+def _case(setup, kind):
+    """(witness bytes, oracle/cpu proof) of one mix, the proof computed once per module."""
     from oracle import cpu_oracle
     circ, zk = setup
     w = circ.witness(91)
     if kind != "natural":
         head, v = _values(w, circ.n_vars)
         w = head + _pattern(kind, v, np.random.default_rng(5)).tobytes()
-    p = zkp_amd.Prover(zk, devices=[0])
+    if kind not in _WANT:
+        _WANT[kind] = cpu_oracle.prove(zk, w, R_FIX, S_FIX, threads=8)[0]
+    return w, _WANT[kind]
+
+
+@pytest.mark.parametrize("kind", ["natural", "all_large", "all_small", "edges"])
+def test_host_witness_proof_equals_oracle(setup, kind):
+    w, want = _case(setup, kind)
+    p = zkp_amd.Prover(setup[1], devices=[0])
     try:
         got, _ = p.prove_raw(w, R_FIX, S_FIX)
         p.stage(w, slot=1)
         staged, _ = p.prove_staged_raw(1, R_FIX, S_FIX)
     finally:
         p.close()
-    want, _ = cpu_oracle.prove(zk, w, R_FIX, S_FIX, threads=8)
     assert got == want
     assert staged == want
+
+
+def test_host_witness_sequence_on_one_prover(setup):
+    """Mixes alternating on one prover: every transfer rewrites the same pinned staging chunks and
+    the device must see the new bytes (a stale chunk from the previous witness gives a wrong proof)."""
+    seq = ["natural", "all_large", "natural", "edges", "all_large", "all_small", "all_large"]
+    p = zkp_amd.Prover(setup[1], devices=[0])
+    try:
+        for i, kind in enumerate(seq):
+            w, want = _case(setup, kind)
+            got, _ = p.prove_raw(w, R_FIX, S_FIX)
+            assert got == want, (i, kind)
+    finally:
+        p.close()

@@ -45,7 +45,10 @@ int main(int argc, char** argv) {
     for (int mix = 0; mix < 4; ++mix) {
       std::vector<uint32_t> v((size_t)n * 8), stage((size_t)wt_chunks(n) * wt_chunk_words(), 0xDEADBEEFu);
       fill(v, n, mix, n * 7 + mix);
-      for (uint32_t c = 0; c < wt_chunks(n); ++c) {
+      // chunks in DESCENDING order: a stray write past a chunk's region would land in the next
+      // chunk, already encoded (the device path encodes chunks on 16 threads in any order)
+      for (uint32_t cc = wt_chunks(n); cc-- > 0;) {
+        const uint32_t c = cc;
         const size_t w = wt_encode_chunk(reinterpret_cast<const uint8_t*>(v.data()), n, c,
                                          stage.data() + (size_t)c * wt_chunk_words());
         if (w > wt_chunk_words() || (w - WT_META_WORDS) % 4) ++bad, printf("chunk size %zu\n", w);

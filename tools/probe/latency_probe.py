@@ -49,6 +49,27 @@ def main():
     el, up, wall = rows[len(rows) // 2]
     print(json.dumps({"host_witness_median_ms": round(el, 3), "upload_ms": round(up, 3), "total_wall_ms": round(wall, 3),
                       "outside_total_wall_ms": round(el - wall, 3)}), flush=True)
+    # the CLI path (snarkjs groth16 prove <zkey> <wtns> <proof> <public>): the witness from a file in
+    # the page cache, proof.json / public.json written
+    import tempfile
+    d = tempfile.mkdtemp()
+    wp = os.path.join(d, "witness.wtns")
+    with open(wp, "wb") as f:
+        f.write(wit)
+    ts = []
+    for _ in range(7):
+        t0 = time.perf_counter()
+        p.prove_files(wp, os.path.join(d, "proof.json"), os.path.join(d, "public.json"))
+        ts.append((time.perf_counter() - t0) * 1e3)
+    ts.sort()
+    t_read = []
+    for _ in range(5):
+        t0 = time.perf_counter()
+        with open(wp, "rb") as f:
+            f.read()
+        t_read.append((time.perf_counter() - t0) * 1e3)
+    print(json.dumps({"prove_files_median_ms": round(ts[len(ts) // 2], 3), "python_file_read_ms": round(min(t_read), 3)}),
+          flush=True)
     p.close()
 
 

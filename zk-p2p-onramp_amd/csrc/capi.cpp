@@ -12,6 +12,11 @@
 #include <string>
 #include <vector>
 
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
 #include "../../include/zkp_amd.h"
 #include "beacon.hpp"
 #include "hip_check.hpp"
@@ -68,6 +73,39 @@ std::vector<uint8_t> read_file(const char* path) {
     throw zkp::ZkpError(ZKP_ERR_IO, std::string("cannot read ") + path);
   return buf;
 }
+
+// A witness file mapped read-only: the prover's transfer threads read the page cache directly (the
+// page faults spread over them) instead of one thread copying 205 MB into a zero-filled buffer
+// first.  Falls back to read_file() where the file cannot be mapped.
+class MappedFile {
+ public:
+  explicit MappedFile(const char* path) {
+    const int fd = ::open(path, O_RDONLY | O_CLOEXEC);
+    if (fd < 0) throw zkp::ZkpError(ZKP_ERR_IO, std::string("cannot open ") + path);
+    struct stat st {};
+    if (::fstat(fd, &st) == 0 && st.st_size > 0) {
+      void* m = ::mmap(nullptr, (size_t)st.st_size, PROT_READ, MAP_PRIVATE, fd, 0);
+      if (m != MAP_FAILED) {
+        map_ = m;
+        len_ = (size_t)st.st_size;
+      }
+    }
+    ::close(fd);
+    if (!map_) copy_ = read_file(path);
+  }
+  ~MappedFile() {
+    if (map_) ::munmap(map_, len_);
+  }
+  MappedFile(const MappedFile&) = delete;
+  MappedFile& operator=(const MappedFile&) = delete;
+  const uint8_t* data() const { return map_ ? static_cast<const uint8_t*>(map_) : copy_.data(); }
+  size_t size() const { return map_ ? len_ : copy_.size(); }
+
+ private:
+  void* map_ = nullptr;
+  size_t len_ = 0;
+  std::vector<uint8_t> copy_;
+};
 
 std::string dec(const uint8_t* le32) { return zkp::host::u256_to_dec(zkp::host::u256_from_le(le32)); }
 
@@ -368,7 +406,7 @@ zkp_status zkp_prove_batch_status(zkp_prover* p, const uint8_t* const* wtns, con
 zkp_status zkp_prove_files(zkp_prover* p, const char* wtns_path, const char* proof_path, const char* public_path) {
   if (!p || !wtns_path || !proof_path || !public_path) return fail(ZKP_ERR_INVALID_ARG, "null argument");
   return guard([&] {
-    std::vector<uint8_t> w = read_file(wtns_path);
+    const MappedFile w(wtns_path);
     const uint32_t npub = p->impl->header().n_public;
     std::vector<uint8_t> pub((size_t)npub * 32 + 32);
     zkp_proof pr{};

@@ -492,11 +492,7 @@ class DevicePipeline {
         (void)hipStreamSynchronize(st);
         std::rethrow_exception(e);
       }
-    // one expansion after every chunk's DMA has completed: kernels enqueued by the encode threads
-    // themselves, each behind its own chunk's DMA on the shared stream, read stale chunk data (a
-    // 4-chunk all-large witness, tests/test_gpu_witness_transfer.py), so the stream order of DMAs
-    // enqueued from several host threads is not relied on
-    HIPX(hipStreamSynchronize(st));
+    // one expansion after every chunk's DMA has been enqueued
     launch_witness_unpack(upstage_[k], 0, n, up_[k], st);
     HIPX(hipStreamSynchronize(st));
     if (pcie_bytes) *pcie_bytes = sent.load();

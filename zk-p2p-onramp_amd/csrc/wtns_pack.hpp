@@ -18,14 +18,20 @@ namespace zkp {
 
 constexpr uint32_t WT_BLOCK = 64, WT_CHUNK_BLOCKS = 1024;
 constexpr size_t WT_META_WORDS = 3 * WT_CHUNK_BLOCKS;  // 12 KiB: payload stays 16-B aligned
-constexpr size_t wt_chunk_words() { return WT_META_WORDS + (size_t)WT_CHUNK_BLOCKS * WT_BLOCK * 8; }  // worst case
+// the branch-free small-word copy of a block with no small lane writes one word past the block's
+// payload: for the chunk's last block that is the first word after the worst-case payload, so every
+// region ends in WT_SLACK spare words (never sent) instead of in the next chunk's metadata, which
+// another thread may already have written
+constexpr size_t WT_SLACK = 4;
+constexpr size_t wt_chunk_words() { return WT_META_WORDS + (size_t)WT_CHUNK_BLOCKS * WT_BLOCK * 8 + WT_SLACK; }
 inline uint32_t wt_blocks(uint32_t n) { return (n + WT_BLOCK - 1) / WT_BLOCK; }
 inline uint32_t wt_chunks(uint32_t n) { return (wt_blocks(n) + WT_CHUNK_BLOCKS - 1) / WT_CHUNK_BLOCKS; }
 
 // encodes chunk c of the n-signal witness at src into its region (wt_chunk_words() words); returns
 // the number of leading words of the region to send.  The stray writes of the branch-free copies
-// stay inside the region: a block's large slots end at most 8 words, its small words at most 1 word,
-// past its own payload, and a block's payload is at most 512 words (all large).
+// stay inside the region: a block's large slots end at most 8 words past its payload when it has a
+// small lane (payload <= 8 L + 64 - L, so still within the 512 words of an all-large block), its
+// small words at most 1 word past it (the last block's: into WT_SLACK).
 inline size_t wt_encode_chunk(const uint8_t* src, uint32_t n, uint32_t c, uint32_t* region) {
   const uint32_t nblk = wt_blocks(n);
   const uint32_t b0 = c * WT_CHUNK_BLOCKS, b1 = nblk < b0 + WT_CHUNK_BLOCKS ? nblk : b0 + WT_CHUNK_BLOCKS;
