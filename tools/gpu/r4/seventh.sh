@@ -1,11 +1,10 @@
-# round 4, seventh call: the witness-transfer tests with the non-coherent pinned staging (diagnosis)
-# and with the coherent one, the whole GPU suite, smoke, the latency probe with the witness file
+# round 4, seventh call:
+# the whole GPU suite, smoke, the latency probe with the witness file
 # mapped (zkp_prove_files) vs read into a buffer, the default bench line, and the same bench under
 # rocprofv3 --kernel-trace --marker-trace with the per-launch split
 set -e
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out/r4
-ZKP_LIB_PATH=$PWD/tools/gpu/r4/libs/lib_noncoh.so timeout -k 10 300 python -u -m pytest tests/test_gpu_witness_transfer.py -v --timeout 120 --timeout-method thread > gpurun_out/r4/gt_noncoh.log 2>&1 || echo "non-coherent staging: failures (see log)"
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/r4/gt_seventh.log 2>&1
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r4/smoke_seventh.log 2>&1
 ZKP_LIB_PATH=$PWD/tools/gpu/r4/libs/lib_readfile.so timeout -k 10 300 python tools/probe/latency_probe.py > gpurun_out/r4/latency_readfile.txt 2> gpurun_out/r4/latency_readfile.err
