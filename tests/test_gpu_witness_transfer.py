@@ -97,3 +97,18 @@ def test_host_witness_sequence_on_one_prover(setup):
             assert got == want, (i, kind)
     finally:
         p.close()
+
+
+def test_batch_of_mixes_on_inflight_pipelines(setup, monkeypatch):
+    """zkp_prove_batch over every mix with two pipelines on the device (ZKP_INFLIGHT=2): transfers of
+    different witnesses into different pipelines' staging run concurrently with proofs."""
+    monkeypatch.setenv("ZKP_INFLIGHT", "2")
+    kinds = ["all_large", "natural", "edges", "all_large", "all_small", "natural", "all_large", "edges"]
+    cases = [_case(setup, k) for k in kinds]
+    p = zkp_amd.Prover(setup[1], devices=[0])
+    try:
+        got = p.prove_batch_raw([w for w, _ in cases], rs=[R_FIX] * len(cases), ss=[S_FIX] * len(cases))
+    finally:
+        p.close()
+    for i, (g, (_, want)) in enumerate(zip(got, cases)):
+        assert g[0] == want, (i, kinds[i])

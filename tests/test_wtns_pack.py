@@ -1,7 +1,8 @@
 """The compact witness transfer format (csrc/wtns_pack.hpp, decoded on the device by qap.hip
 k_witness_unpack): tools/hosttest/wtns_pack_test encodes witnesses of uniform, all-small, 70 %
 small and lane-pattern mixes (2^32, 2^32 - 1, top-word-only values, whole blocks of one kind) at
-sizes 1, 63, 64, 65, 64K, 3 x 64K + 37 and 4 x 64K, decodes every signal the way the kernel does and
+sizes 1, 63, 64, 65, 64K, 128K - 1, 3 x 64K + 37, 4 x 64K and four random ones (chunks encoded in descending or
+shuffled order), decodes every signal the way the kernel does and
 compares it with the input.  CPU-only; the GPU side is tests/test_gpu_witness_transfer.py."""
 import os
 import shutil

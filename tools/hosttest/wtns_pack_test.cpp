@@ -2,6 +2,7 @@
 // several value mixes chunk by chunk, decodes every signal as k_witness_unpack does (wt_decode_one)
 // and compares with the input; then times the encoder over a Venmo-sized witness with T threads.
 // usage: wtns_pack_test [n] [threads]   (prints "ok" lines and one timing line per mix)
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -41,14 +42,20 @@ int main(int argc, char** argv) {
   const uint32_t nbig = argc > 1 ? (uint32_t)atoi(argv[1]) : 6400000;
   const int T = argc > 2 ? atoi(argv[2]) : 4;
   int bad = 0;
-  for (uint32_t n : {1u, 63u, 64u, 65u, 65536u, 3u * 65536 + 37, 4u * 65536}) {
+  std::mt19937_64 sizes(12345);
+  std::vector<uint32_t> ns = {1u, 63u, 64u, 65u, 65536u, 65536u * 2 - 1, 3u * 65536 + 37, 4u * 65536};
+  for (int r = 0; r < 4; ++r) ns.push_back(1 + (uint32_t)(sizes() % (5u * 65536)));
+  for (uint32_t n : ns) {
     for (int mix = 0; mix < 4; ++mix) {
       std::vector<uint32_t> v((size_t)n * 8), stage((size_t)wt_chunks(n) * wt_chunk_words(), 0xDEADBEEFu);
       fill(v, n, mix, n * 7 + mix);
-      // chunks in DESCENDING order: a stray write past a chunk's region would land in the next
-      // chunk, already encoded (the device path encodes chunks on 16 threads in any order)
-      for (uint32_t cc = wt_chunks(n); cc-- > 0;) {
-        const uint32_t c = cc;
+      // chunks in DESCENDING (mixes 0, 2) or shuffled (mixes 1, 3) order: a stray write past a chunk's
+      // region would land in a chunk already encoded (the device path encodes chunks on 16 threads in
+      // any order)
+      std::vector<uint32_t> order(wt_chunks(n));
+      for (uint32_t c = 0; c < order.size(); ++c) order[c] = (uint32_t)order.size() - 1 - c;
+      if (mix & 1) std::shuffle(order.begin(), order.end(), sizes);
+      for (uint32_t c : order) {
         const size_t w = wt_encode_chunk(reinterpret_cast<const uint8_t*>(v.data()), n, c,
                                          stage.data() + (size_t)c * wt_chunk_words());
         if (w > wt_chunk_words() || (w - WT_META_WORDS) % 4) ++bad, printf("chunk size %zu\n", w);

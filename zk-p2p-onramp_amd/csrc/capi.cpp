@@ -250,6 +250,8 @@ zkp_status zkp_beacon_secret(const uint8_t* beacon, size_t len, uint32_t num_ite
   return guard([&] { zkp::beacon_secret(beacon, len, num_iterations_exp, k32); });
 }
 
+}  // extern "C"
+
 namespace {
 // one phase-2 contribution drawn from rng: the record appended to section 10 (mpc.cpp), then the
 // group arithmetic on the GPU (delta -> k delta, L and H -> k^-1) and the new section 10
@@ -266,6 +268,7 @@ std::vector<uint8_t> contribute_mpc(int device, const uint8_t* zkey, size_t len,
   return buf;
 }
 }  // namespace
+extern "C" {
 
 zkp_status zkp_zkey_beacon_named(int device, const uint8_t* zkey, size_t len, const uint8_t* beacon, size_t beacon_len,
                                  uint32_t num_iterations_exp, const char* name, uint8_t** out, size_t* out_len) {
@@ -450,6 +453,8 @@ zkp_status zkp_prover_set_verify(zkp_prover* p, int on) {
   return guard([&] { p->impl->set_verify(on != 0); });
 }
 
+}  // extern "C"
+
 namespace {
 using zkp::host::Affine;
 using HFq = zkp::host::Fq;
@@ -473,6 +478,7 @@ Affine<HFq2> g2_std(const uint8_t* b) {
   return Affine<HFq2>{HFq2{fq_std(b), fq_std(b + 32)}, HFq2{fq_std(b + 64), fq_std(b + 96)}, false};
 }
 }  // namespace
+extern "C" {
 
 zkp_status zkp_proof_verify(const uint8_t* zkey, size_t len, const zkp_proof* proof, int* valid) {
   if (!zkey || !proof || !valid) return fail(ZKP_ERR_INVALID_ARG, "null argument");
