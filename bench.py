@@ -66,7 +66,18 @@ def load_traffic():
     """Newest committed PMC summary of the accumulate kernel.  HBM bytes per launch = FETCH_SIZE +
     WRITE_SIZE: the kernel's bytes are random 64-B base gathers, for which FETCH_SIZE counts the
     bytes exactly (profiles/fetch_calibration_r02.json; the x2 of coalesced 16-B streams does not
-    apply).  Older summaries that stored 2 x FETCH_SIZE are recomputed from their raw counters."""
+    apply).  Round 4's summary is per launch kind (the H launch, the roofline's); older summaries
+    averaged every G1 launch and are recomputed from their raw counters."""
+    p = os.path.join(ROOT, "profiles", "pmc_launch_r04.json")
+    try:
+        with open(p) as f:
+            h = json.load(f)["kinds"]["H"]
+        return {"hbm_bytes_per_launch": h["hbm_bytes_per_dispatch"],
+                "valu_lane_instructions_per_addition": h.get("valu_lane_instructions_per_addition"),
+                "source": "profiles/pmc_launch_r04.json (the H launch: rocprofv3 --pmc FETCH_SIZE x1 + WRITE_SIZE, "
+                          "gather-calibrated; tools/prof/pmc_launch.py)"}
+    except Exception:
+        pass
     for name in ("pmc_accumulate_r03.json", "pmc_accumulate_r02.json", "pmc_accumulate_r01.json"):
         p = os.path.join(ROOT, "profiles", name)
         try:
@@ -377,6 +388,7 @@ def accumulate_rooflines(launches, peak, peak_src, traffic):
         "algorithmic_work_per_launch": {"mixed_adds": h.get("mixed_adds_per_launch"), "fp_mul_per_add": FPMUL_PER_MADD,
                                         "mac_per_fp_mul": MAC_PER_FPMUL},
         "valu_issue_frac_pmc": traffic.get("valu_issue_frac") if traffic else None,
+        "valu_lane_instructions_per_addition_pmc": traffic.get("valu_lane_instructions_per_addition") if traffic else None,
         "avg_launch_ms": h.get("avg_launch_ms"),
         "launches_timed": h.get("launches"),
         "peak_source": peak_src,
