@@ -18,20 +18,17 @@ namespace zkp {
 
 constexpr uint32_t WT_BLOCK = 64, WT_CHUNK_BLOCKS = 1024;
 constexpr size_t WT_META_WORDS = 3 * WT_CHUNK_BLOCKS;  // 12 KiB: payload stays 16-B aligned
-// the branch-free small-word copy of a block with no small lane writes one word past the block's
-// payload: for the chunk's last block that is the first word after the worst-case payload, so every
-// region ends in WT_SLACK spare words (never sent) instead of in the next chunk's metadata, which
-// another thread may already have written
+// every region ends in WT_SLACK spare words (never sent): round 4's first encoder wrote one word past
+// an all-large block, which for a chunk's last block was the next chunk's metadata, possibly already
+// written by another thread; the encoder now stores only inside each block's payload
 constexpr size_t WT_SLACK = 4;
 constexpr size_t wt_chunk_words() { return WT_META_WORDS + (size_t)WT_CHUNK_BLOCKS * WT_BLOCK * 8 + WT_SLACK; }
 inline uint32_t wt_blocks(uint32_t n) { return (n + WT_BLOCK - 1) / WT_BLOCK; }
 inline uint32_t wt_chunks(uint32_t n) { return (wt_blocks(n) + WT_CHUNK_BLOCKS - 1) / WT_CHUNK_BLOCKS; }
 
 // encodes chunk c of the n-signal witness at src into its region (wt_chunk_words() words); returns
-// the number of leading words of the region to send.  The stray writes of the branch-free copies
-// stay inside the region: a block's large slots end at most 8 words past its payload when it has a
-// small lane (payload <= 8 L + 64 - L, so still within the 512 words of an all-large block), its
-// small words at most 1 word past it (the last block's: into WT_SLACK).
+// the number of leading words of the region to send.  Every store lands inside the block's own
+// payload (no stray writes; the slack words are kept as a guard).
 inline size_t wt_encode_chunk(const uint8_t* src, uint32_t n, uint32_t c, uint32_t* region) {
   const uint32_t nblk = wt_blocks(n);
   const uint32_t b0 = c * WT_CHUNK_BLOCKS, b1 = nblk < b0 + WT_CHUNK_BLOCKS ? nblk : b0 + WT_CHUNK_BLOCKS;
@@ -41,39 +38,38 @@ inline size_t wt_encode_chunk(const uint8_t* src, uint32_t n, uint32_t c, uint32
   for (uint32_t b = b0; b < b1; ++b) {
     const uint32_t i0 = b * WT_BLOCK, m = n - i0 < WT_BLOCK ? n - i0 : WT_BLOCK;
     const uint8_t* v = src + (size_t)i0 * 32;
-    // branch-free (a 0/1-heavy witness mixes the kinds unpredictably): the small-lane mask from
-    // 16-B compares, then the large values to consecutive 32-B slots (each lane writes its slot, a
-    // small lane's is overwritten by the next large one or by the small words), then the low words
+    // the small-lane mask from 16-B compares, then the large values and the small low words each
+    // walked over the set bits of their lane mask (no per-lane branch on the kind: a 0/1-heavy
+    // witness mixes them unpredictably) and written with non-temporal stores: the staging is
+    // write-once memory read by the DMA engine, so no cache line is read for ownership first
     const __m128i hi3 = _mm_set_epi32(-1, -1, -1, 0), zero = _mm_setzero_si128();
-    uint64_t mask = m < WT_BLOCK ? ~0ull << m : 0ull;
+    const uint64_t valid = m < WT_BLOCK ? (1ull << m) - 1 : ~0ull;
+    uint64_t mask = ~valid;
     for (uint32_t l = 0; l < m; ++l) {
       const __m128i a = _mm_loadu_si128(reinterpret_cast<const __m128i*>(v + 32 * l));
       const __m128i c = _mm_loadu_si128(reinterpret_cast<const __m128i*>(v + 32 * l + 16));
       const __m128i o = _mm_or_si128(_mm_and_si128(a, hi3), c);
       mask |= (uint64_t)(_mm_movemask_epi8(_mm_cmpeq_epi32(o, zero)) == 0xFFFF) << l;
     }
-    const uint32_t L = WT_BLOCK - (uint32_t)__builtin_popcountll(mask);
-    uint32_t* big = pay + off;
-    for (uint32_t l = 0; l < m; ++l) {
-      _mm_storeu_si128(reinterpret_cast<__m128i*>(big), _mm_loadu_si128(reinterpret_cast<const __m128i*>(v + 32 * l)));
-      _mm_storeu_si128(reinterpret_cast<__m128i*>(big + 4),
-                       _mm_loadu_si128(reinterpret_cast<const __m128i*>(v + 32 * l + 16)));
-      big += 8 * (uint32_t)(~(mask >> l) & 1u);
+    __m128i* out = reinterpret_cast<__m128i*>(pay + off);  // 16-B aligned: offsets are multiples of 4 words
+    uint32_t L = 0;
+    for (uint64_t bm = ~mask; bm; bm &= bm - 1, ++L) {
+      const uint8_t* x = v + 32 * (uint32_t)__builtin_ctzll(bm);
+      _mm_stream_si128(out++, _mm_loadu_si128(reinterpret_cast<const __m128i*>(x)));
+      _mm_stream_si128(out++, _mm_loadu_si128(reinterpret_cast<const __m128i*>(x + 16)));
     }
-    uint32_t* small = pay + off + 8 * L;
+    alignas(16) uint32_t lo[WT_BLOCK + 3];
     uint32_t ns = 0;
-    for (uint32_t l = 0; l < m; ++l) {
-      uint32_t x;
-      std::memcpy(&x, v + 32 * l, 4);
-      small[ns] = x;
-      ns += (uint32_t)(mask >> l) & 1u;
-    }
+    for (uint64_t sm = mask & valid; sm; sm &= sm - 1) std::memcpy(&lo[ns++], v + 32 * (uint32_t)__builtin_ctzll(sm), 4);
+    for (uint32_t k = ns; k < ((ns + 3) & ~3u); ++k) lo[k] = 0;
+    for (uint32_t k = 0; k < ns; k += 4) _mm_stream_si128(out++, _mm_load_si128(reinterpret_cast<const __m128i*>(lo + k)));
     uint32_t* mb = meta + 3 * (size_t)(b - b0);
     mb[0] = (uint32_t)mask;
     mb[1] = (uint32_t)(mask >> 32);
     mb[2] = off;
     off += (8 * L + ns + 3) & ~3u;
   }
+  _mm_sfence();  // the non-temporal stores are globally visible before the chunk's DMA is enqueued
   return WT_META_WORDS + off;
 }
 
