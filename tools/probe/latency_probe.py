@@ -38,6 +38,33 @@ def main():
     for gap in (0, 0.003, 0.05):
         med, mn = staged(gap)
         print(json.dumps({"staged_gap_ms": gap * 1e3, "median_ms": med, "min_ms": mn}), flush=True)
+    if os.environ.get("LATENCY_PROBE_GAP_MODES"):
+        # what the idle-gap penalty is made of: the 3 ms gap spent spinning on the host CPU, or with the
+        # GPU kept busy by 256 MB device memsets (hipMemsetAsync on the null stream, one per 0.25 ms)
+        import ctypes
+        hip = ctypes.CDLL("libamdhip64.so")
+        buf = ctypes.c_void_p()
+        assert hip.hipMalloc(ctypes.byref(buf), ctypes.c_size_t(256 << 20)) == 0
+
+        def gap_mode(mode, n=8):
+            ts = []
+            for _ in range(n):
+                t_end = time.perf_counter() + 0.003
+                while time.perf_counter() < t_end:
+                    if mode == "gpu_busy":
+                        hip.hipMemsetAsync(buf, ctypes.c_int(0), ctypes.c_size_t(256 << 20), None)
+                        t_next = time.perf_counter() + 0.00025
+                        while time.perf_counter() < t_next:
+                            pass
+                hip.hipDeviceSynchronize()
+                t0 = time.perf_counter()
+                p.prove_staged_raw(0, R_FIX, S_FIX)
+                ts.append((time.perf_counter() - t0) * 1e3)
+            return round(statistics.median(ts), 3), round(min(ts), 3)
+        for mode in ("cpu_spin", "gpu_busy"):
+            med, mn = gap_mode(mode)
+            print(json.dumps({"staged_gap_ms": 3.0, "gap_mode": mode, "median_ms": med, "min_ms": mn}), flush=True)
+        hip.hipFree(buf)
     rows = []
     for _ in range(7):
         t0 = time.perf_counter()
