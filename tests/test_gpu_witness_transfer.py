@@ -1,6 +1,6 @@
 """The compact witness transfer (prover.hip DevicePipeline::upload + qap.hip k_witness_unpack): the
-host sends each block of 64 signals as its values >= 2^32 (32 B) and the low words of the others,
-the device expands them.  A proof from a host witness must equal oracle/cpu's proof of the same
+host sends each block of 64 signals as its 0 / 1 values in the block metadata, its values >= 2^32
+(32 B) and the low words of the others; the device expands them.  A proof from a host witness must equal oracle/cpu's proof of the same
 witness at the same r, s, whatever the mix of small and large values and wherever they sit in their
 block; the witnesses here span several 64K-signal chunks and end in a ragged block.  Witnesses other
 than the circuit's own do not satisfy it: the proof is still a deterministic function of (key,
@@ -36,6 +36,15 @@ def _pattern(kind, v, rng):
     elif kind == "all_small":
         v[:] = 0
         v[:, 0] = rng.integers(0, 1 << 32, size=n, dtype=np.uint64).astype(np.uint32)
+    elif kind == "bits":
+        # 0 / 1 values (carried in the block metadata) beside uniform ones, lane by lane at random
+        r = rng.integers(0, 1 << 32, size=v.shape, dtype=np.uint64).astype(np.uint32)
+        r[:, 7] &= 0x1FFFFFFF
+        b = rng.integers(0, 2, size=n, dtype=np.uint32)
+        isbit = rng.integers(0, 10, size=n) < 7
+        v[:] = r
+        v[isbit] = 0
+        v[isbit, 0] = b[isbit]
     elif kind == "edges":
         # per lane: 0, 2^32 - 1 (small), 2^32 (large), only the top word set (large), 1, random
         k = np.arange(n) % 6
@@ -71,7 +80,7 @@ def _case(setup, kind):
     return w, _WANT[kind]
 
 
-@pytest.mark.parametrize("kind", ["natural", "all_large", "all_small", "edges"])
+@pytest.mark.parametrize("kind", ["natural", "all_large", "all_small", "bits", "edges"])
 def test_host_witness_proof_equals_oracle(setup, kind):
     w, want = _case(setup, kind)
     p = zkp_amd.Prover(setup[1], devices=[0])
@@ -88,7 +97,7 @@ def test_host_witness_proof_equals_oracle(setup, kind):
 def test_host_witness_sequence_on_one_prover(setup):
     """Mixes alternating on one prover: every transfer rewrites the same pinned staging chunks and
     the device must see the new bytes (a stale chunk from the previous witness gives a wrong proof)."""
-    seq = ["natural", "all_large", "natural", "edges", "all_large", "all_small", "all_large"]
+    seq = ["natural", "all_large", "natural", "edges", "all_large", "bits", "all_small", "all_large"]
     p = zkp_amd.Prover(setup[1], devices=[0])
     try:
         for i, kind in enumerate(seq):
@@ -103,7 +112,7 @@ def test_batch_of_mixes_on_inflight_pipelines(setup, monkeypatch):
     """zkp_prove_batch over every mix with two pipelines on the device (ZKP_INFLIGHT=2): transfers of
     different witnesses into different pipelines' staging run concurrently with proofs."""
     monkeypatch.setenv("ZKP_INFLIGHT", "2")
-    kinds = ["all_large", "natural", "edges", "all_large", "all_small", "natural", "all_large", "edges"]
+    kinds = ["all_large", "natural", "edges", "bits", "all_small", "natural", "all_large", "edges"]
     cases = [_case(setup, k) for k in kinds]
     p = zkp_amd.Prover(setup[1], devices=[0])
     try:

@@ -90,19 +90,21 @@ __global__ __launch_bounds__(TPB) void k_witness_unpack(const uint32_t* __restri
   if (i >= n) return;
   const uint32_t g = i / WT_BLOCK, lane = i % WT_BLOCK;
   const uint32_t* region = stage + (size_t)(g / WT_CHUNK_BLOCKS) * wt_chunk_words();
-  const uint32_t* mb = region + 3 * (size_t)(g % WT_CHUNK_BLOCKS);
-  const uint64_t mask = (uint64_t)mb[0] | ((uint64_t)mb[1] << 32);
-  const uint64_t below = lane ? mask & (~0ull >> (64 - lane)) : 0ull;
-  const uint32_t ns = (uint32_t)__popcll(below), nl = lane - ns, L = WT_BLOCK - (uint32_t)__popcll(mask);
-  const uint32_t* blk = region + WT_META_WORDS + mb[2];
+  const uint32_t* mb = region + WT_META_PER_BLOCK * (size_t)(g % WT_CHUNK_BLOCKS);
+  const uint64_t smallm = (uint64_t)mb[0] | ((uint64_t)mb[1] << 32), bitm = (uint64_t)mb[2] | ((uint64_t)mb[3] << 32),
+                 bitv = (uint64_t)mb[4] | ((uint64_t)mb[5] << 32), large = ~(smallm | bitm);
+  const uint64_t below = lane ? ~0ull >> (64 - lane) : 0ull;
+  const uint32_t* blk = region + WT_META_WORDS + mb[6];
   uint4* o = reinterpret_cast<uint4*>(out + (size_t)i * 8);
-  if ((mask >> lane) & 1u) {
-    o[0] = make_uint4(blk[8 * L + ns], 0u, 0u, 0u);
-    o[1] = make_uint4(0u, 0u, 0u, 0u);
-  } else {
-    const uint4* q = reinterpret_cast<const uint4*>(blk + 8 * nl);  // block offsets are multiples of 4 words
+  if ((large >> lane) & 1u) {
+    const uint4* q = reinterpret_cast<const uint4*>(blk + 8 * __popcll(large & below));  // 16-B aligned
     o[0] = q[0];
     o[1] = q[1];
+  } else {
+    const uint32_t x = ((bitm >> lane) & 1u) ? (uint32_t)(bitv >> lane) & 1u
+                                             : blk[8 * __popcll(large) + __popcll(smallm & below)];
+    o[0] = make_uint4(x, 0u, 0u, 0u);
+    o[1] = make_uint4(0u, 0u, 0u, 0u);
   }
 }
 
