@@ -335,8 +335,9 @@ def batch_pcie_inclusive(args, circ, prover, wit, refs, rank, world, ndev, dist,
             "check": "every batch proof == a separately computed proof of the same witness at the same r, s",
             "pipelines_per_device": int(os.environ.get("ZKP_INFLIGHT", "1")),
             "workers_per_pipeline": 2,
-            "note": "zkp_prove_batch from pageable host memory over %d device(s): the 205 MB witness upload of "
-                    "proof i+1 (pinned slot, copy stream) runs while proof i computes" % ndev}
+            "note": "zkp_prove_batch from pageable host memory over %d device(s): the compact transfer of "
+                    "witness i+1 (16 encode threads, pinned staging, 4 copy queues) runs while proof i computes"
+                    % ndev}
 
 
 def roctx():
@@ -672,9 +673,11 @@ def main():
                            "pcie_bytes": int(max(up_mb) * 1e6),
                            "witness_GBps": round(wit_bytes / (upload_ms * 1e-3) / 1e9, 1) if upload_ms > 0 else None,
                            "host_encode_threads": 16,
-                           "note": "compact transfer: 16 host threads encode 64K-signal chunks (values < 2^32 as one "
-                                   "word) into pinned memory, each chunk's DMA overlapping the next chunk's encoding, "
-                                   "one kernel expands them in HBM; ms = pageable witness -> 32-B layout in HBM"},
+                           "note": "compact transfer: 16 host threads encode 64K-signal chunks (0/1 values as "
+                                   "metadata bits, other values < 2^32 as one word) into pinned memory with "
+                                   "non-temporal stores, each chunk's DMA on one of 4 copy queues as soon as it is "
+                                   "encoded, one kernel expands them in HBM; ms = pageable witness -> 32-B layout "
+                                   "in HBM"},
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
