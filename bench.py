@@ -315,7 +315,10 @@ def batch_pcie_inclusive(args, circ, prover, wit, refs, rank, world, ndev, dist,
     host = (list(wit) + extra)[:k]
     ref = list(refs[:len(host)]) + [prover.prove_raw(w, r_fix, s_fix) for w in host[len(refs):]]
     order = [i % k for i in range(args.batch)]
-    prover.prove_batch_raw(host[:2], [r_fix] * 2, [s_fix] * 2)
+    # untimed warm-up batch: two proofs per worker (2 workers x ZKP_INFLIGHT pipelines x devices), so
+    # every pipeline, upload slot and encode thread has run before the timed batch
+    nwarm = 2 * 2 * int(os.environ.get("ZKP_INFLIGHT", "1")) * ndev
+    prover.prove_batch_raw([host[i % k] for i in range(nwarm)], [r_fix] * nwarm, [s_fix] * nwarm)
     if dist:
         dist.barrier()
     sync()
@@ -470,8 +473,8 @@ def cpu_baseline(args, zk, wit0, gpu_proof, r_fix, s_fix, msm_case):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=8)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--witnesses", type=int, default=4, help="distinct staged witnesses per rank (cycled)")
     ap.add_argument("--cpu-baseline", choices=["full", "none"], default="full")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every usable host core (nproc, cgroup quota)")
