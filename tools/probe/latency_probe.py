@@ -64,6 +64,22 @@ def main():
         for mode in ("cpu_spin", "gpu_busy"):
             med, mn = gap_mode(mode)
             print(json.dumps({"staged_gap_ms": 3.0, "gap_mode": mode, "median_ms": med, "min_ms": mn}), flush=True)
+        # every other host core kept busy (14 spinning child processes at the lowest priority) through
+        # idle 3-ms gaps: if the penalty goes away, it is the host's idle states
+        import subprocess
+        kids = [subprocess.Popen([sys.executable, "-c", "import os\nos.nice(19)\nwhile True: pass"]) for _ in range(14)]
+        try:
+            time.sleep(0.5)
+            med, mn = staged(0.003)
+            print(json.dumps({"staged_gap_ms": 3.0, "gap_mode": "host_cores_busy", "median_ms": med, "min_ms": mn}),
+                  flush=True)
+            med, mn = staged(0)
+            print(json.dumps({"staged_gap_ms": 0.0, "gap_mode": "host_cores_busy", "median_ms": med, "min_ms": mn}),
+                  flush=True)
+        finally:
+            for k in kids:
+                k.kill()
+                k.wait()
         hip.hipFree(buf)
     rows = []
     for _ in range(7):
