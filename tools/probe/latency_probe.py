@@ -40,7 +40,8 @@ def main():
         print(json.dumps({"staged_gap_ms": gap * 1e3, "median_ms": med, "min_ms": mn}), flush=True)
     if os.environ.get("LATENCY_PROBE_GAP_MODES"):
         # what the idle-gap penalty is made of: the 3 ms gap spent spinning on the host CPU, or with the
-        # GPU kept busy by 256 MB device memsets (hipMemsetAsync on the null stream, one per 0.25 ms)
+        # GPU kept busy by device memsets (hipMemsetAsync on the null stream, one per 0.25 ms) of 256 MB
+        # (evicting the caches) or of 4 KB
         import ctypes
         hip = ctypes.CDLL("libamdhip64.so")
         buf = ctypes.c_void_p()
@@ -51,8 +52,10 @@ def main():
             for _ in range(n):
                 t_end = time.perf_counter() + 0.003
                 while time.perf_counter() < t_end:
-                    if mode == "gpu_busy":
-                        hip.hipMemsetAsync(buf, ctypes.c_int(0), ctypes.c_size_t(256 << 20), None)
+                    if mode in ("gpu_busy", "gpu_tiny"):
+                        # gpu_tiny: 4-KB memsets keep the device from idling without evicting its caches
+                        size = (256 << 20) if mode == "gpu_busy" else 4096
+                        hip.hipMemsetAsync(buf, ctypes.c_int(0), ctypes.c_size_t(size), None)
                         t_next = time.perf_counter() + 0.00025
                         while time.perf_counter() < t_next:
                             pass
@@ -61,7 +64,7 @@ def main():
                 p.prove_staged_raw(0, R_FIX, S_FIX)
                 ts.append((time.perf_counter() - t0) * 1e3)
             return round(statistics.median(ts), 3), round(min(ts), 3)
-        for mode in ("cpu_spin", "gpu_busy"):
+        for mode in ("cpu_spin", "gpu_busy", "gpu_tiny"):
             med, mn = gap_mode(mode)
             print(json.dumps({"staged_gap_ms": 3.0, "gap_mode": mode, "median_ms": med, "min_ms": mn}), flush=True)
         # every other host core kept busy (14 spinning child processes at the lowest priority) through
