@@ -164,6 +164,10 @@ def kernel_benches(device, log_n=20, iters=10):
     # proof loop is ~5 % slower than a cold one on the same box: clocks)
     ntt_ms = min(zkp_amd.bench_ntt(log_n, warmup=3, iters=20, device=device) for _ in range(3))
     ntt23_ms = min(zkp_amd.bench_ntt(23, warmup=3, iters=20, device=device) for _ in range(3))
+    # the batched extension of three vectors (every pass one launch over all three: the split
+    # quotient stage runs this; the proof keeps one vector per launch, DESIGN.md §5 NTT), per vector
+    b20 = min(zkp_amd.bench_ntt(log_n, warmup=3, iters=20, device=device, count=3) for _ in range(3)) / 3
+    b23 = min(zkp_amd.bench_ntt(23, warmup=3, iters=20, device=device, count=3) for _ in range(3)) / 3
     return {
         "msm_g1_2^20_ms": round(st["ms_per_msm"], 3),
         "msm_g1_2^20_result_check": "equal to the c=13/T=1 MSM of the same input",
@@ -171,7 +175,9 @@ def kernel_benches(device, log_n=20, iters=10):
         "msm_g1_2^20_accumulate_ms": round(st["ms_accumulate"], 3),
         "msm_window_bits": st["c"],
         "ntt_fr_2^20_coset_extend_ms": round(ntt_ms, 3),
-        "ntt_roofline": {"2^20": ntt_roofline(log_n, ntt_ms), "2^23 (Venmo domain)": ntt_roofline(23, ntt23_ms)},
+        "ntt_roofline": {"2^20": ntt_roofline(log_n, ntt_ms), "2^23 (Venmo domain)": ntt_roofline(23, ntt23_ms),
+                         "2^20 batched x3, per vector": ntt_roofline(log_n, b20),
+                         "2^23 batched x3, per vector": ntt_roofline(23, b23)},
     }, st, (pts, scal, res)
 
 

@@ -293,6 +293,9 @@ zkp_status zkp_bench_plan(int device, const uint8_t* scalars, size_t n, int wind
                           int iters, double* ms);
 /* ms per coset-extension (iNTT + coset key + NTT) of 2^log_n Fr elements */
 zkp_status zkp_bench_ntt(int device, int log_n, int warmup, int iters, double* ms);
+/* ms per batched coset-extension of count (1..3) vectors of 2^log_n Fr elements, every pass one
+ * launch over all of them: what the prover runs on the quotient's A, B, C */
+zkp_status zkp_bench_ntt_batch(int device, int log_n, int count, int warmup, int iters, double* ms);
 
 #ifdef __cplusplus
 }

@@ -50,6 +50,10 @@ def test_version_and_error_before_device():
     with pytest.raises(zkp_amd.ZkpError) as e:
         zkp_amd.ntt_fr([1, 2, 3], 0)
     assert e.value.status == 1
+    for count in (0, 4):  # the batched coset extension takes 1..3 vectors
+        with pytest.raises(zkp_amd.ZkpError) as e:
+            zkp_amd.bench_ntt(10, count=count)
+        assert e.value.status == 1
 
 
 def test_proof_json_formatting_matches_snarkjs():

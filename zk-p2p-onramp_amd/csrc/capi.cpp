@@ -605,7 +605,12 @@ zkp_status zkp_bench_plan(int device, const uint8_t* scalars, size_t n, int wind
 
 zkp_status zkp_bench_ntt(int device, int log_n, int warmup, int iters, double* ms) {
   if (!ms || log_n < 1 || log_n > 27) return fail(ZKP_ERR_INVALID_ARG, "bad argument");
-  return guard([&] { *ms = zkp::bench_ntt(device, log_n, warmup, iters); });
+  return guard([&] { *ms = zkp::bench_ntt(device, log_n, 1, warmup, iters); });
+}
+
+zkp_status zkp_bench_ntt_batch(int device, int log_n, int count, int warmup, int iters, double* ms) {
+  if (!ms || log_n < 1 || log_n > 27 || count < 1 || count > 3) return fail(ZKP_ERR_INVALID_ARG, "bad argument");
+  return guard([&] { *ms = zkp::bench_ntt(device, log_n, count, warmup, iters); });
 }
 
 }  // extern "C"

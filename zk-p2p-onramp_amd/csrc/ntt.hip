@@ -42,6 +42,17 @@ struct Tile {
   int lm, b, lc, lbt;
 };
 
+// the vectors of one launch (coset_extend_batch: A, B and C of the quotient in one grid): workgroup
+// w works on tile w mod 2^lt of vector w >> lt, so a pass over three vectors is one launch of 3x the
+// tiles -- 2^20's 1024 tiles per vector over 768 resident workgroups leave a third of a round
+// half-idle per launch, 3072 fill four rounds
+struct Polys {
+  uint32_t* p0;
+  uint32_t* p1;
+  uint32_t* p2;
+  int lt;  // log2 tiles per vector
+};
+
 // the stage roots of a b-bit pass, precomputed once per (direction, b) in their LDS layout
 // (k_root_table): staging is a copy (no products per root per workgroup)
 __device__ __forceinline__ void stage_roots(uint32_t* __restrict__ ltw, const uint32_t* __restrict__ rtab) {
@@ -213,13 +224,14 @@ __device__ __forceinline__ int brev_src(const Tile& T, int e) {
 // tw: w_(2^lm)^(col*row) by position in block (null when n2 == 1).  rootsA / rootsB: the stage
 // roots (the k_root_table of this b and direction), B for MODE 2's forward DFT.
 template <int MODE, int LE>
-__global__ __launch_bounds__(NTT_TPB) void k_ntt(uint32_t* __restrict__ data, Tile T, const uint32_t* __restrict__ tw,
+__global__ __launch_bounds__(NTT_TPB) void k_ntt(Polys P, Tile T, const uint32_t* __restrict__ tw,
                                              const uint32_t* __restrict__ rootsA, const uint32_t* __restrict__ rootsB,
                                              const uint32_t* __restrict__ coset) {
   __shared__ uint32_t lds[NL << LOG_TILE];  // SoA: lds[limb * E + element]
   __shared__ __attribute__((aligned(16))) uint32_t ltw[RW * MAX_TW];
   const int E = LE ? (1 << LE) : (1 << (T.b + T.lc + T.lbt));  // LE: the tile size known at compile time
-  const uint32_t tile = blockIdx.x;
+  const uint32_t vec = blockIdx.x >> P.lt, tile = blockIdx.x & ((1u << P.lt) - 1);
+  uint32_t* __restrict__ data = vec == 0 ? P.p0 : (vec == 1 ? P.p1 : P.p2);
   stage_roots(ltw, rootsA);
   constexpr int VPT = (1 << LOG_TILE) / NTT_TPB;  // elements per thread of a full tile
   if (LE && MODE == 1 && tw) {
@@ -545,11 +557,14 @@ NttEngine::~NttEngine() {
       if (p) (void)hipFree(p);
 }
 
-// mode 0: DIF pass p, 1: DIT (transposed) pass p, 2: fused innermost pass (inverse then forward)
-void NttEngine::launch_pass(uint32_t* data, int mode, int p, bool inv) {
+// mode 0: DIF pass p, 1: DIT (transposed) pass p, 2: fused innermost pass (inverse then forward);
+// over count (1..3) vectors in one grid
+void NttEngine::launch_pass(uint32_t* const* data, int count, int mode, int p, bool inv) {
   const int k = log_n_;
   const Tile T = make_tile(k, lms_[p], bits_[p]);
-  const size_t tiles = (size_t(1) << k) >> (T.b + T.lc + T.lbt);
+  const int lt = k - (T.b + T.lc + T.lbt);
+  const size_t tiles = (size_t)count << lt;
+  const Polys P{data[0], count > 1 ? data[1] : data[0], count > 2 ? data[2] : data[0], lt};
   const int d = inv ? 1 : 0;
   const uint32_t *ra = rtab_[d][T.b], *rinv = rtab_[1][T.b], *rfwd = rtab_[0][T.b];
   const uint32_t* none = nullptr;
@@ -559,20 +574,20 @@ void NttEngine::launch_pass(uint32_t* data, int mode, int p, bool inv) {
   auto k1 = full ? k_ntt<1, LOG_TILE> : k_ntt<1, 0>;
   auto k2 = full ? k_ntt<2, LOG_TILE> : k_ntt<2, 0>;
   if (mode == 0)
-    hipLaunchKernelGGL(k0, dim3((unsigned)tiles), dim3(NTT_TPB), 0, stream_, data, T, tw_pass_[d][p], ra, none, none);
+    hipLaunchKernelGGL(k0, dim3((unsigned)tiles), dim3(NTT_TPB), 0, stream_, P, T, tw_pass_[d][p], ra, none, none);
   else if (mode == 1)
-    hipLaunchKernelGGL(k1, dim3((unsigned)tiles), dim3(NTT_TPB), 0, stream_, data, T, tw_pass_[d][p], ra, none, none);
+    hipLaunchKernelGGL(k1, dim3((unsigned)tiles), dim3(NTT_TPB), 0, stream_, P, T, tw_pass_[d][p], ra, none, none);
   else
-    hipLaunchKernelGGL(k2, dim3((unsigned)tiles), dim3(NTT_TPB), 0, stream_, data, T, none, rinv, rfwd, coset_pos_);
+    hipLaunchKernelGGL(k2, dim3((unsigned)tiles), dim3(NTT_TPB), 0, stream_, P, T, none, rinv, rfwd, coset_pos_);
 }
 
-void NttEngine::dif_passes(uint32_t* data, bool inv, int first, int last) {
-  for (int p = first; p < last; ++p) launch_pass(data, 0, p, inv);
+void NttEngine::dif_passes(uint32_t* const* data, int count, bool inv, int first, int last) {
+  for (int p = first; p < last; ++p) launch_pass(data, count, 0, p, inv);
 }
 
-void NttEngine::dit_passes(uint32_t* data, bool inv, int first, int last) {
+void NttEngine::dit_passes(uint32_t* const* data, int count, bool inv, int first, int last) {
   // transposed passes in reverse order: block sizes grow back from the innermost
-  for (int p = last - 1; p >= first; --p) launch_pass(data, 1, p, inv);
+  for (int p = last - 1; p >= first; --p) launch_pass(data, count, 1, p, inv);
 }
 
 void NttEngine::scale(uint32_t* data, int mode) {
@@ -589,28 +604,31 @@ void NttEngine::digit_reverse(uint32_t* data, bool to_natural) {
                      log_n_, make_pb(bits_), to_natural ? 1 : 0);
 }
 
-void NttEngine::coset_extend(uint32_t* data) {
+void NttEngine::coset_extend_batch(uint32_t* const* data, int count) {
+  if (count < 1 || count > 3) throw std::invalid_argument("coset_extend_batch: 1..3 vectors");
   if (log_n_ == 0) {
     // n = 1: coefficient = value; evaluation at g is the same constant
     return;
   }
   const int P = (int)bits_.size();
-  dif_passes(data, true, 0, P - 1);  // inverse, outer passes
-  launch_pass(data, 2, P - 1, true);  // innermost inverse pass + coset key + innermost forward pass
-  dit_passes(data, false, 0, P - 1);  // forward, outer passes (transposed, reverse order)
+  dif_passes(data, count, true, 0, P - 1);  // inverse, outer passes
+  launch_pass(data, count, 2, P - 1, true);  // innermost inverse pass + coset key + innermost forward pass
+  dit_passes(data, count, false, 0, P - 1);  // forward, outer passes (transposed, reverse order)
   HIPX(hipGetLastError());
 }
 
+void NttEngine::coset_extend(uint32_t* data) { coset_extend_batch(&data, 1); }
+
 void NttEngine::forward(uint32_t* data) {
   if (log_n_ == 0) return;
-  dif_passes(data, false, 0, (int)bits_.size());
+  dif_passes(&data, 1, false, 0, (int)bits_.size());
   digit_reverse(data, true);
   HIPX(hipGetLastError());
 }
 
 void NttEngine::inverse(uint32_t* data) {
   if (log_n_ == 0) return;
-  dif_passes(data, true, 0, (int)bits_.size());
+  dif_passes(&data, 1, true, 0, (int)bits_.size());
   scale(data, 1);
   digit_reverse(data, true);
   HIPX(hipGetLastError());

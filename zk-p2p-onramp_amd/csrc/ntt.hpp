@@ -36,6 +36,9 @@ class NttEngine {
   // data: n Fr elements, device layout (Montgomery R' = 2^261, 8 LE words each)
   // natural-order evaluations on <w>  ->  natural-order evaluations on g<w>
   void coset_extend(uint32_t* data);
+  // the same for count (1..3) vectors of n elements each, every pass one launch over all of them
+  // (the quotient's A, B, C)
+  void coset_extend_batch(uint32_t* const* data, int count);
   // plain transforms (natural in, natural out), for tests
   void forward(uint32_t* data);  // A_j = sum a_i w^(ij)
   void inverse(uint32_t* data);  // a_i = n^-1 sum A_j w^(-ij)
@@ -45,9 +48,9 @@ class NttEngine {
  private:
   // passes [first, last) of the DIF sequence (dir 1 = inverse root), resp. of the
   // transposed DIT sequence in reverse order
-  void dif_passes(uint32_t* data, bool inv, int first, int last);
-  void dit_passes(uint32_t* data, bool inv, int first, int last);
-  void launch_pass(uint32_t* data, int mode, int p, bool inv);
+  void dif_passes(uint32_t* const* data, int count, bool inv, int first, int last);
+  void dit_passes(uint32_t* const* data, int count, bool inv, int first, int last);
+  void launch_pass(uint32_t* const* data, int count, int mode, int p, bool inv);
   void scale(uint32_t* data, int mode);  // 0: x g^f(pos)/n   1: x 1/n (digit-reversed layout ok)
   void digit_reverse(uint32_t* data, bool to_natural);
   int log_n_;

@@ -539,6 +539,10 @@ class DevicePipeline {
     launch_build_abc(rowptr_[0], col_[0], val_[0], rowptr_[1], col_[1], val_[1], d_wit, h.domain_size, abc_[0],
                      abc_[1], abc_[2], s0_);
     HIPX(hipEventRecord(ev_[2], s0_));
+    // one vector per launch, not coset_extend_batch: the batched passes (3x the workgroups at s0's
+    // high priority) finish the quotient ~1.8 ms sooner but crowd out the G2 and witness
+    // accumulations that fill the per-vector launches' last-round gaps -- -4 % proofs/s, +0.5 ms
+    // latency on one box, 4 alternating rounds (profiles/ntt_batch_ab_r04.txt)
     for (auto* b : abc_) ntt_->coset_extend(b);
     launch_join_abc(abc_[0], abc_[1], abc_[2], h.domain_size, pscal_, s0_);
     HIPX(hipEventRecord(ev_[3], s0_));
@@ -614,12 +618,17 @@ class DevicePipeline {
     const ZkeyHeader& h = hdr_;
     launch_build_abc(rowptr_[0], col_[0], val_[0], rowptr_[1], col_[1], val_[1], d, h.domain_size, abc_[0], abc_[1],
                      abc_[2], s0_);
+    uint32_t* sel[3];
+    int cnt = 0;
     for (int v = 0; v < 3; ++v) {
       if (!(mask >> v & 1)) continue;
       if (!dst[v]) throw ZkpError(ZKP_ERR_INVALID_ARG, "quotient part: null destination");
-      ntt_->coset_extend(abc_[v]);
-      HIPX(hipMemcpyAsync(dst[v], abc_[v], (size_t)h.domain_size * 32, hipMemcpyDeviceToDevice, s0_));
+      sel[cnt++] = abc_[v];
     }
+    if (cnt) ntt_->coset_extend_batch(sel, cnt);
+    for (int v = 0; v < 3; ++v)
+      if (mask >> v & 1)
+        HIPX(hipMemcpyAsync(dst[v], abc_[v], (size_t)h.domain_size * 32, hipMemcpyDeviceToDevice, s0_));
     HIPX(hipStreamSynchronize(s0_));
   }
 
@@ -1545,8 +1554,10 @@ float bench_plan(int device, const uint8_t* scalars, size_t n, int c, int dense,
   return ms / iters;
 }
 
-float bench_ntt(int device, int log_n, int warmup, int iters) {
+float bench_ntt(int device, int log_n, int count, int warmup, int iters) {
   if (iters <= 0) throw ZkpError(ZKP_ERR_INVALID_ARG, "bench_ntt: iters must be > 0");
+  if (count < 1 || count > 3) throw ZkpError(ZKP_ERR_INVALID_ARG, "bench_ntt: 1..3 vectors");
+  if (log_n < 0 || log_n > 27) throw ZkpError(ZKP_ERR_INVALID_ARG, "bench_ntt: log_n out of range");
   HIPX(hipSetDevice(device));
   hipStream_t st;
   HIPX(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
@@ -1558,8 +1569,7 @@ float bench_ntt(int device, int log_n, int warmup, int iters) {
   float ms = 0;
   try {
     NttEngine eng(log_n, st);
-    HIPX(hipMalloc(&d, n * 32));
-    HIPX(hipMemsetAsync(d, 0x11, n * 32, st));  // any values < 2^256 with top bits clear work
+    HIPX(hipMalloc(&d, n * 32 * count));
     std::vector<uint32_t> seed(n * 8);
     uint64_t x = 0x5A4B5032;
     for (auto& v : seed) {  // uniform-ish Fr-sized values
@@ -1567,10 +1577,15 @@ float bench_ntt(int device, int log_n, int warmup, int iters) {
       v = (uint32_t)(x >> 32);
     }
     for (size_t i = 0; i < n; ++i) seed[i * 8 + 7] &= 0x0fffffffu;
-    HIPX(hipMemcpyAsync(d, seed.data(), n * 32, hipMemcpyHostToDevice, st));
-    for (int i = 0; i < warmup; ++i) eng.coset_extend(d);
+    uint32_t* vecs[3];
+    for (int v = 0; v < count; ++v) {
+      vecs[v] = d + (size_t)v * n * 8;
+      HIPX(hipMemcpyAsync(vecs[v], seed.data(), n * 32, hipMemcpyHostToDevice, st));
+    }
+    HIPX(hipStreamSynchronize(st));  // seed is released at the end of the scope
+    for (int i = 0; i < warmup; ++i) eng.coset_extend_batch(vecs, count);
     HIPX(hipEventRecord(e0, st));
-    for (int i = 0; i < iters; ++i) eng.coset_extend(d);
+    for (int i = 0; i < iters; ++i) eng.coset_extend_batch(vecs, count);
     HIPX(hipEventRecord(e1, st));
     HIPX(hipEventSynchronize(e1));
     HIPX(hipEventElapsedTime(&ms, e0, e1));

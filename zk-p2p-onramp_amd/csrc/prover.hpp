@@ -164,8 +164,8 @@ struct MsmBench {
 };
 MsmBench bench_msm(int device, Curve curve, const uint8_t* points, const uint8_t* scalars, size_t n, int warmup,
                    int iters, uint8_t* out, int* is_inf);
-// ms per coset_extend (iNTT + coset key + NTT) of 2^log_n Fr elements
-float bench_ntt(int device, int log_n, int warmup, int iters);
+// ms per coset_extend_batch (iNTT + coset key + NTT) of count vectors of 2^log_n Fr elements
+float bench_ntt(int device, int log_n, int count, int warmup, int iters);
 // ms per MsmPlan::build (digits + bucket grouping + task offsets) of n scalars, window bits c (0 = auto),
 // dense (every digit an entry: the H plan) or compacted
 float bench_plan(int device, const uint8_t* scalars, size_t n, int c, int dense, int warmup, int iters);

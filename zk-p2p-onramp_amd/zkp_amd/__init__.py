@@ -106,6 +106,8 @@ def load_library(path: str = LIB_PATH):
                                       ctypes.POINTER(ctypes.c_double), u8p, ctypes.POINTER(ctypes.c_int)]
         lib.zkp_bench_ntt.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                       ctypes.POINTER(ctypes.c_double)]
+        lib.zkp_bench_ntt_batch.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                            ctypes.POINTER(ctypes.c_double)]
         lib.zkp_bench_plan.argtypes = [ctypes.c_int, u8p, sz, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                        ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
         lib.zkp_msm.argtypes = [ctypes.c_int, ctypes.c_int, u8p, u8p, sz, ctypes.c_int, ctypes.c_int, u8p,
@@ -144,7 +146,7 @@ def load_library(path: str = LIB_PATH):
                      "zkp_prover_timings", "zkp_msm_g1", "zkp_msm_g2", "zkp_ntt_fr", "zkp_quotient",
                      "zkp_witness_stage", "zkp_prove_staged", "zkp_prover_instrument", "zkp_prover_kernel_stats",
                      "zkp_prover_launch_stats",
-                     "zkp_bench_msm", "zkp_bench_ntt", "zkp_bench_plan", "zkp_msm", "zkp_prover_msm_config",
+                     "zkp_bench_msm", "zkp_bench_ntt", "zkp_bench_ntt_batch", "zkp_bench_plan", "zkp_msm", "zkp_prover_msm_config",
                      "zkp_prover_load_part", "zkp_prove_partial", "zkp_proof_calldata",
                      "zkp_prover_load_chunks", "zkp_zkey_read", "zkp_zkey_read_chunks", "zkp_zkey_contribute", "zkp_zkey_new",
                      "zkp_beacon_secret", "zkp_zkey_beacon", "zkp_prove_partial_staged", "zkp_proof_combine",
@@ -761,7 +763,12 @@ def bench_plan(scalars_le: bytes, window_bits: int = 0, dense: bool = True, warm
     return ms.value
 
 
-def bench_ntt(log_n: int, warmup: int = 2, iters: int = 10, device: int = 0) -> float:
+def bench_ntt(log_n: int, warmup: int = 2, iters: int = 10, device: int = 0, count: int = 1) -> float:
+    """ms per coset extension of `count` (1..3) vectors of 2^log_n elements, every pass one launch
+    over all of them (count 3 is the prover's A, B, C)."""
     ms = ctypes.c_double()
-    _check(load_library().zkp_bench_ntt(device, log_n, warmup, iters, ctypes.byref(ms)))
+    if count == 1:
+        _check(load_library().zkp_bench_ntt(device, log_n, warmup, iters, ctypes.byref(ms)))
+    else:
+        _check(load_library().zkp_bench_ntt_batch(device, log_n, count, warmup, iters, ctypes.byref(ms)))
     return ms.value
