@@ -66,3 +66,34 @@ def test_split_distributed_quotient(name, nparts, balance, monkeypatch):
     assert parts == _oracle_partials(zk, wt, nparts, balance)
     (a, b, c), _ = zkp_amd.proof_combine_raw(zk, parts, wt, r, s)
     assert {"A": a, "B": b, "C": c} == want
+
+
+@pytest.mark.parametrize("name", ["small", "venmo_mini", "synth_2^14"])
+def test_batched_coset_extension_equals_per_vector(name):
+    # zkp_quotient_part_staged extends the vectors of its mask in one launch per pass
+    # (NttEngine::coset_extend_batch, workgroup w: tile w mod 2^lt of the w >> lt-th vector); every
+    # mask must give the same bytes per vector as extending that vector alone
+    import torch
+    if name.startswith("synth"):  # full 1024-element tiles, 16 per vector
+        from zkp_amd import synth
+        circ = synth.Circuit(9000, (1 << 14) - 40, 5, 0x5A4B5032)
+        zk, wt = circ.zkey(0x5A4B5033).bytes(), circ.witness(7)
+    else:
+        zk, wt, r, s, want = _case(name)
+    p = zkp_amd.Prover(zk, devices=[0], part=0, nparts=1)
+    try:
+        n = p.domain_size
+        p.stage(wt, 0)
+        alone = []
+        for v in range(3):
+            t = torch.empty(n * 32, dtype=torch.uint8, device="cuda")
+            p.quotient_part_staged(0, 1 << v, [t.data_ptr() if u == v else None for u in range(3)])
+            alone.append(t.cpu())
+        for mask in (7, 5, 6, 3):
+            out = [torch.full((n * 32,), 0xA5, dtype=torch.uint8, device="cuda") for _ in range(3)]
+            p.quotient_part_staged(0, mask, [out[v].data_ptr() if mask >> v & 1 else None for v in range(3)])
+            for v in range(3):
+                if mask >> v & 1:
+                    assert torch.equal(out[v].cpu(), alone[v]), (mask, v)
+    finally:
+        p.close()
