@@ -23,3 +23,15 @@ def test_launch_split_reproduces_bench_fracs(tmp_path):
     for kind, v in res["kinds"].items():
         assert v["dispatches"] == v["bench_launches"], kind
         assert abs(v["frac_delta"]) <= 0.03, (kind, v)
+
+
+def test_ntt_issue_rate_recomputes_from_committed_counters():
+    """DESIGN §5 NTT: the 2^20 / 2^23 roofline ratio factors into credited
+    products per instruction x issue rate; tools/prof/ntt_issue.py over the committed (k_ntt rows
+    only) kernel traces and SQ counter passes reproduces profiles/ntt_issue_r04.json."""
+    res = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "prof", "ntt_issue.py"),
+                          os.path.join(P, "ntt_issue_r04")], check=True, capture_output=True, text=True, timeout=120)
+    got = json.loads(res.stdout)
+    assert got == json.load(open(os.path.join(P, "ntt_issue_r04.json")))
+    r = got["ratio_20_over_23"]
+    assert 0.95 < r["products_per_instr"] < 1.0 and r["issue_rate"] < 0.85
