@@ -338,7 +338,10 @@ def batch_pcie_inclusive(args, circ, prover, wit, refs, rank, world, ndev, dist,
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     bad = [j for j in range(len(order)) if j >= len(res) or res[j] != ref[order[j]]]
+    vmode = prover.verify_mode()
     return {"proofs_per_rank": len(order), "distinct_host_witnesses": k, "n_gpus": world * ndev,
+            "verify_before_return_mode": vmode,
+            "verified": "%d/%d" % (len(res) if vmode != 0 else 0, len(order)),
             "proofs_per_s": round(len(order) * world / el, 3), "ms_per_proof": round(el / len(order) * 1e3, 3),
             "all_proofs_ok": len(res) == len(order) and not bad, "mismatched_proofs": bad[:8],
             "check": "every batch proof == a separately computed proof of the same witness at the same r, s",

@@ -196,14 +196,18 @@ zkp_status zkp_prover_timings(const zkp_prover* p, float* ms, int n);
 void zkp_prover_free(zkp_prover* p);
 
 /* Verify-before-return (the reference verifies every proof right after proving:
- * dizkus-scripts/5_gen_proof.sh:14-21 `snarkjs groth16 verify`).  on != 0: every proof of
- * zkp_prove / zkp_prove_batch[_status] / zkp_prove_staged / zkp_prove_files is checked on the
- * host (optimal-ate pairing, the Verifier.sol:340-358 equation) against the zkey's verification
- * key before it is returned; a proof that fails the check is never returned: the call reports
- * ZKP_ERR_INTERNAL ("proof failed verify-before-return ...").  Default: off, or on when the
- * environment holds ZKP_VERIFY=1 at load.  Cost: a few ms of one host core per proof (batch:
- * on the worker thread, overlapping the next proof). */
+ * dizkus-scripts/5_gen_proof.sh:14-21 `snarkjs groth16 verify`).  A checked proof is verified on
+ * the host (optimal-ate pairing, the Verifier.sol:340-358 equation) against the zkey's verification
+ * key before it is returned; a proof that fails the check is never returned: the call (or that
+ * proof's batch status) reports ZKP_ERR_INTERNAL ("proof failed verify-before-return ...").
+ * on = 0: off; 1: every proof of zkp_prove / zkp_prove_batch[_status] / zkp_prove_staged /
+ * zkp_prove_files; 2 (the DEFAULT): the proofs of zkp_prove_batch[_status] only -- there the check
+ * runs on the worker thread while the next proof computes (no measured throughput cost), while on
+ * a single proof it would add a few ms of one host core to the latency.  The environment
+ * ZKP_VERIFY=0/1/2 at load overrides the default.  Any other nonzero `on` means 1. */
 zkp_status zkp_prover_set_verify(zkp_prover* p, int on);
+/* The current verify-before-return mode (0, 1 or 2 as above). */
+zkp_status zkp_prover_get_verify(const zkp_prover* p, int* mode);
 
 /* Host only (no device): `snarkjs groth16 verify` of one proof against a zkey's verification key
  * (sections 2 and 3).  *valid = 1 if the proof verifies (public signals from proof->public_signals,

@@ -5,7 +5,10 @@ A silent device error is injected with the test hook ZKP_TEST_CORRUPT_H=1 (the H
 by one generator): with verification off the prover returns a proof that the restated
 Verifier.sol rejects; with it on (zkp_prover_set_verify, or ZKP_VERIFY=1 at load) the proof is
 never returned -- zkp_prove, zkp_prove_staged and every proof of a batch report ZKP_ERR_INTERNAL.
-Healthy proofs pass the check unchanged (bit-exact golden proofs) and report its host cost."""
+Healthy proofs pass the check unchanged (bit-exact golden proofs) and report its host cost.
+The default (mode 2) checks every batch proof and no single proof: with ZKP_TEST_CORRUPT_H=2 (only
+the odd-indexed proofs of a batch corrupted) the default batch refuses exactly those and proves
+the rest."""
 import json
 import os
 
@@ -66,4 +69,24 @@ def test_verify_env_default(golden_dir, monkeypatch):
     with pytest.raises(zkp_amd.ZkpError) as e:
         p.prove_raw(wt, r, s)
     assert e.value.status == ERR_INTERNAL
+    p.close()
+
+
+def test_default_batch_refuses_corrupt_proves_rest(golden_dir, monkeypatch):
+    monkeypatch.delenv("ZKP_VERIFY", raising=False)
+    monkeypatch.setenv("ZKP_TEST_CORRUPT_H", "2")
+    zk, wt, r, s, want = _case(golden_dir, "venmo_mini")
+    p = zkp_amd.Prover(zk)
+    assert p.verify_mode() == zkp_amd.Prover.VERIFY_BATCH
+    res, st = p.prove_batch_status_raw([wt] * 6, [r] * 6, [s] * 6)
+    assert st == [0, ERR_INTERNAL] * 3
+    for i in (0, 2, 4):
+        assert groth16.js_stringify(zkp_amd.proof_object(*res[i][0])) == want
+    assert res[1] is None and res[3] is None and res[5] is None
+    # single proofs are not checked by default (mode 2): a single proof is never corrupted by hook 2
+    assert groth16.js_stringify(p.prove(wt, r=r, s=s)["proof"]) == want
+    p.set_verify(False)
+    res, st = p.prove_batch_status_raw([wt] * 2, [r] * 2, [s] * 2)
+    assert st == [0, 0]  # verification off: the corrupted proof goes out unchecked ...
+    assert not zkp_amd.proof_verify(zk, *res[1])  # ... and the verifier rejects it
     p.close()

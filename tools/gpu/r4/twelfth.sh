@@ -1,5 +1,7 @@
 # round 4, twelfth call: non-temporal bit-walk encoder vs the branch-free one: the encoder alone on
 # the box's CPU, the transfer tests, and the latency probe alternating (3 rounds)
+# (historical: wtns_pack_test_old_bin was the encoder test of the revision before c4fbc20, built
+# here with `git show c4fbc20^:zk-p2p-onramp_amd/csrc/wtns_pack.hpp` in place; it is no longer tracked)
 set -e
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out/r4

@@ -113,6 +113,27 @@ def main(n=300):
         wq = (wv << 261) // R
         lines.append("shoupr %s %s %s" % (l9(a, raw=k % 2 == 1), w8(wv), l9(wq)))
         checks.append(("shoupr", lambda z, a=a, wv=wv: z % R == a * wv % R and z < 3 * R))
+    # round-5 NTT unit (ntt.hip r4_unit, field.hpp sub_raw6n): tile values < 3r normalised, at the value
+    # extreme (3r - 1) and at the limb extreme (every low limb 2^29 - 1, top limb just below 3r's);
+    # tw a table value < 2r (Montgomery), w a plain root < r with its Shoup quotient
+    lowmax = (1 << 232) - 1
+    x3e = [0, 1, 3 * R - 1, lowmax + ((((3 * R - 1) >> 232) - 1) << 232), lowmax, 2 * R - 1]
+    twe = [2 * R - 1, lowmax + ((((2 * R - 1) >> 232) - 1) << 232), 1]
+    quads4 = [[rnd.randrange(3 * R) for _ in range(4)] for _ in range(n)]
+    quads4 += [[a, b, c, d] for a in x3e for b in x3e for c in x3e[2:4] for d in x3e[2:4]]
+    quads4 += [[a, b, c, d] for a in x3e[2:4] for b in x3e[2:4] for c in x3e for d in x3e]
+    for k, (x0, x1, x2, x3) in enumerate(quads4):
+        wv = R - 1 if k % 3 == 0 else rnd.randrange(R)
+        tw = twe[k % 3] if k % 2 == 0 else rnd.randrange(2 * R)
+        wq = (wv << 261) // R
+        lines.append("r4lazy %s %s %s %s %s %s %s" % (w8(x0), w8(x1), w8(x2), w8(x3), w8(wv), l9(wq), w8(tw)))
+        s02, s13 = x0 + x2, x1 + x3
+        checks.append(("r4lazy_y1", lambda z, t=(s02 - s13) * wv: z % R == t % R and z < 3 * R))
+        checks.append(("r4lazy_p1", lambda z, t=s02 - s13: z % R == t % R and z < 6 * R // 5))
+        checks.append(("r4lazy_p0tw", lambda z, t=(s02 + s13) * tw: z % R == t * inv_rp_r % R and z < 2 * R))
+        checks.append(("r4lazy_p1tw", lambda z, t=(s02 - s13) * tw: z % R == t * inv_rp_r % R and z < 2 * R))
+        checks.append(("r4lazy_p2tw", lambda z, t=(x0 + x2) * tw: z % R == t * inv_rp_r % R and z < 2 * R))
+        checks.append(("r4lazy_p3tw", lambda z, t=(x0 - x2) * tw: z % R == t * inv_rp_r % R and z < 2 * R))
     # Shoup quotients of the NTT's stage roots (field.hpp shoup_quot) and sub4 against inputs < 4r
     RP_ = 1 << 261
     for wm in [0, 1, R - 1, R - 2] + [rnd.randrange(R) for _ in range(n)]:

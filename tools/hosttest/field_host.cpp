@@ -42,6 +42,18 @@ int main() {
       const Fr s02 = add_raw(x0, x2), s13 = add_raw(x1, x3);
       prf(add_raw_reduce(s02, s13)); printf("\n"); prf(mul(sub_raw6(s02, s13), w));
     }
+    else if (o == "r4lazy") {  // round-5 NTT unit forms (ntt.hip r4_unit): x0..x3 < 3m normalised,
+      // w plain root (words) with its Shoup quotient wq (limbs), tw a table value < 2m (words)
+      Fr x0 = rdf<FrCfg>(), x1 = rdf<FrCfg>(), x2 = rdf<FrCfg>(), x3 = rdf<FrCfg>(), w = rdf<FrCfg>();
+      Fr wq = rdl<FrCfg>(), tw = rdf<FrCfg>();
+      const Fr s02 = add_raw(x0, x2), s13 = add_raw(x1, x3);
+      prf(mul_shoup(sub_raw6n(s02, s13), w, wq)); printf("\n");   // full unit: y1 (< 3m)
+      prf(qreduce(sub_raw6n(s02, s13))); printf("\n");            // stored last pair: p1 (< 1.2m)
+      prf(mul(add_raw(s02, s13), tw)); printf("\n");              // raw last pair p0 x twiddle (< 2m)
+      prf(mul(sub_raw6n(s02, s13), tw)); printf("\n");            // raw p1 x twiddle
+      prf(mul(add_raw(x0, x2), tw)); printf("\n");                // raw p2 (d02 + d13, each < 3m)
+      prf(mul(rsub(x0, x2), tw));                                  // raw p3 / odd stage x - y + 4m
+    }
     else if (o == "shoupr") {  // a (limbs), w (words, plain), wq (limbs): a w mod r in [0, 3r)
       Fr a = rdl<FrCfg>(), w = rdf<FrCfg>(), wq = rdl<FrCfg>();
       prf(mul_shoup(a, w, wq));

@@ -450,7 +450,13 @@ void zkp_prover_free(zkp_prover* p) {
 
 zkp_status zkp_prover_set_verify(zkp_prover* p, int on) {
   if (!p || !p->impl) return fail(ZKP_ERR_INVALID_ARG, "null prover");
-  return guard([&] { p->impl->set_verify(on != 0); });
+  return guard([&] { p->impl->set_verify(on == 0 ? 0 : (on == 2 ? 2 : 1)); });
+}
+
+zkp_status zkp_prover_get_verify(const zkp_prover* p, int* mode) {
+  if (!p || !p->impl || !mode) return fail(ZKP_ERR_INVALID_ARG, "null argument");
+  *mode = p->impl->verify_mode();
+  return ZKP_OK;
 }
 
 }  // extern "C"

@@ -126,10 +126,17 @@ __device__ __forceinline__ void root_mul_pair(const Fr& a, uint32_t ja, const Fr
 }
 
 // one radix-4 unit (thread work item q) of round t: rows r0 + {0, H/2, H, 3H/2} of stage t
-// (span H) and t+1 (span H/2), r0 = grp 2H + i
+// (span H) and t+1 (span H/2), r0 = grp 2H + i.
+// Value bounds (round 5, host-tested: tools/hosttest op r4lazy): every tile value between rounds is
+// normalised (limbs < 2^29) and < 3m (Shoup outputs < 3m, qreduce outputs < 1.2m).  The first-stage
+// sums stay raw (< 6m, limbs < 2^30); their difference takes the 2^30-raised 6m borrow form without a
+// carry pass (sub_raw6n: limbs < 2.5 * 2^30, < 12m), a mul_shoup operand.  RAW: the unit is the last
+// one of a DFT whose outputs only feed a Montgomery product (the DIF pass's inter-pass twiddle, the
+// coset key between the fused kernel's two DFTs): its four outputs stay unreduced (< 12m, limbs
+// < 2.5 * 2^30 -- a mul() operand against the normalised table value), 4 reductions fewer.
 template <int LE>
 __device__ __forceinline__ void r4_unit(uint32_t* __restrict__ lds, const uint32_t* __restrict__ ltw, int E, int b,
-                                        int lc, int t, int q) {
+                                        int lc, int t, int q, bool raw) {
   const uint32_t C = 1u << lc;
   const int lhalf = b - 1 - t;
   const uint32_t Hh = 1u << (lhalf - 1);
@@ -150,32 +157,38 @@ __device__ __forceinline__ void r4_unit(uint32_t* __restrict__ lds, const uint32
   const uint32_t j = i << (t + 1);
   Fr d02, d13;
   root_mul_pair(rsub(x0, x2), i << t, rsub(x1, x3), (i + Hh) << t, ltw, d02, d13);
-  if (Hh > 1) {  // the sums stay raw (< 4m) and meet one reduction
-    const Fr s02 = add_raw(x0, x2), s13 = add_raw(x1, x3);
+  const Fr s02 = add_raw(x0, x2), s13 = add_raw(x1, x3);  // < 6m, limbs < 2^30
+  if (Hh > 1) {
     lds_put<LE>(lds, E, p0, add_raw_reduce(s02, s13));
     Fr y1, y3;
-    root_mul_pair(sub_raw6(s02, s13), j, rsub(d02, d13), j, ltw, y1, y3);
+    root_mul_pair(sub_raw6n(s02, s13), j, rsub(d02, d13), j, ltw, y1, y3);
     lds_put<LE>(lds, E, p1, y1);
     lds_put<LE>(lds, E, p3, y3);
-  } else {  // last pair (span 1): no multiply in stage t+1
-    const Fr s02 = add(x0, x2), s13 = add(x1, x3);
-    lds_put<LE>(lds, E, p0, add(s02, s13));
-    lds_put<LE>(lds, E, p1, sub(s02, s13));
+    lds_put<LE>(lds, E, p2, add(d02, d13));
+  } else if (raw) {  // last pair (span 1, no multiply in stage t+1), outputs into a Montgomery product
+    lds_put<LE>(lds, E, p0, add_raw(s02, s13));    // < 12m, limbs < 2^31
+    lds_put<LE>(lds, E, p1, sub_raw6n(s02, s13));  // < 12m, limbs < 2.5 * 2^30
+    lds_put<LE>(lds, E, p2, add_raw(d02, d13));    // < 6m, limbs < 2^30
+    lds_put<LE>(lds, E, p3, rsub(d02, d13));       // < 7m, limbs < 1.5 * 2^30
+  } else {  // last pair, outputs stored: one reduction each
+    lds_put<LE>(lds, E, p0, add_raw_reduce(s02, s13));
+    lds_put<LE>(lds, E, p1, qreduce(sub_raw6n(s02, s13)));
+    lds_put<LE>(lds, E, p2, add(d02, d13));
     lds_put<LE>(lds, E, p3, stage_sub(d02, d13));
   }
-  lds_put<LE>(lds, E, p2, add(d02, d13));
 }
 
 // b radix-2 DIF stages on the LDS tile (rows natural in, bit-reversed out), done two at a
-// time as radix-4 groups in registers (half the LDS traffic and barriers of radix-2)
+// time as radix-4 groups in registers (half the LDS traffic and barriers of radix-2).  raw: the
+// outputs feed a Montgomery product only (r4_unit)
 template <int LE>
 __device__ __forceinline__ void dft_stages(uint32_t* __restrict__ lds, const uint32_t* __restrict__ ltw, int E_rt,
-                                           int b, int lc) {
+                                           int b, int lc, bool raw) {
   const int E = LE ? (1 << LE) : E_rt;
   const uint32_t C = 1u << lc;
   int t = 0;
   for (; t + 1 < b; t += 2) {
-    for (int q = threadIdx.x; q < (E >> 2); q += NTT_TPB) r4_unit<LE>(lds, ltw, E, b, lc, t, q);
+    for (int q = threadIdx.x; q < (E >> 2); q += NTT_TPB) r4_unit<LE>(lds, ltw, E, b, lc, t, q, raw);
     __syncthreads();
   }
   if (t < b) {  // odd b: the last radix-2 stage (span 1)
@@ -184,8 +197,13 @@ __device__ __forceinline__ void dft_stages(uint32_t* __restrict__ lds, const uin
       const uint32_t bl = (uint32_t)q >> (lc + b - 1);
       const int p0 = swz((int)(bl << (b + lc)) + (int)((bq << 1) << lc) + (int)col), p1 = p0 ^ swz((int)C);
       const Fr x = lds_get<LE>(lds, E, p0), y = lds_get<LE>(lds, E, p1);
-      lds_put<LE>(lds, E, p0, add(x, y));
-      lds_put<LE>(lds, E, p1, stage_sub(x, y));  // span 1: the root is w_2^0 = 1
+      if (raw) {  // < 6m and < 7m, into a Montgomery product
+        lds_put<LE>(lds, E, p0, add_raw(x, y));
+        lds_put<LE>(lds, E, p1, rsub(x, y));
+      } else {
+        lds_put<LE>(lds, E, p0, add(x, y));
+        lds_put<LE>(lds, E, p1, stage_sub(x, y));  // span 1: the root is w_2^0 = 1
+      }
     }
     __syncthreads();
   }
@@ -264,7 +282,8 @@ __global__ __launch_bounds__(NTT_TPB) void k_ntt(Polys P, Tile T, const uint32_t
     }
   }
   __syncthreads();
-  dft_stages<LE>(lds, ltw, E, T.b, T.lc);
+  // raw last round: MODE 0's outputs meet the inter-pass twiddle, MODE 2's first DFT the coset key
+  dft_stages<LE>(lds, ltw, E, T.b, T.lc, MODE == 2 || (MODE == 0 && tw != nullptr));
   if (MODE == 2) {
     // output row k1 (natural position in the block) sits at LDS row brev(k1): key it with
     // g^f(pos)/n and put it back at row k1 as the forward DFT's input
@@ -315,7 +334,7 @@ __global__ __launch_bounds__(NTT_TPB) void k_ntt(Polys P, Tile T, const uint32_t
       }
     }
     __syncthreads();
-    dft_stages<LE>(lds, ltw, E, T.b, T.lc);
+    dft_stages<LE>(lds, ltw, E, T.b, T.lc, false);
   }
   if (LE && MODE == 0 && tw) {
 #pragma unroll

@@ -928,8 +928,11 @@ Prover::Prover(const uint8_t* zkey, size_t len, const std::vector<int>& devices,
   }
   // test hooks (never set in production): verify-before-return default, a corrupted H partial
   // (exercises verify-before-return), an injected device failure (exercises the batch re-queue)
-  verify_.store(env_int("ZKP_VERIFY", 0) == 1);
-  corrupt_h_ = env_int("ZKP_TEST_CORRUPT_H", 0) == 1;
+  {
+    const int v = env_int("ZKP_VERIFY", 2);
+    verify_.store(v >= 0 && v <= 2 ? v : 2);
+  }
+  corrupt_h_ = env_int("ZKP_TEST_CORRUPT_H", 0);
   // ZKP_TEST_FAIL="<pipeline>:<after>": that pipeline reports a device failure from its (after+1)-th proof on
   if (const char* f = std::getenv("ZKP_TEST_FAIL")) {
     int fp = -1, after = 0;
@@ -1167,7 +1170,7 @@ void Prover::prove(const uint8_t* wtns, size_t len, const uint8_t* r32, const ui
     throw;
   }
   auto t1 = std::chrono::steady_clock::now();
-  assemble_post(hdr_, bl, maybe_corrupt(m.h, corrupt_h_), w, out);
+  assemble_post(hdr_, bl, maybe_corrupt(m.h, corrupt_h_ == 1), w, out);
   auto t2 = std::chrono::steady_clock::now();
   const float vms = verify() ? verify_or_throw(w, out) : 0.f;
   std::lock_guard<std::mutex> lk(tmu_);
@@ -1232,8 +1235,8 @@ zkp_status Prover::prove_batch(const uint8_t* const* wtns, const size_t* lens, i
         DevicePipeline::MsmOut m = d.prove(w, [&](const DevicePipeline::MsmOut& o) {
           bl = assemble_pre(hdr_, o, r32s ? r32s[i] : nullptr, s32s ? s32s[i] : nullptr);
         });
-        assemble_post(hdr_, bl, maybe_corrupt(m.h, corrupt_h_), w, &outs[i]);
-        if (verify()) verify_or_throw(w, &outs[i]);  // on the worker thread: overlaps the next proof
+        assemble_post(hdr_, bl, maybe_corrupt(m.h, corrupt_h_ == 1 || (corrupt_h_ == 2 && (i & 1))), w, &outs[i]);
+        if (verify_batch()) verify_or_throw(w, &outs[i]);  // on the worker thread: overlaps the next proof
         finish(i, ZKP_OK, "");
       } catch (const HipError& e) {
         retire_device(d);  // every pipeline of that device (ZKP_INFLIGHT siblings share its state)
@@ -1343,7 +1346,7 @@ void Prover::prove_staged(int dev, int slot, const uint8_t* r32, const uint8_t* 
     w.values = staged_pub_[dev][slot].data();
     w.n_witness = hdr_.n_vars;
   }
-  assemble_post(hdr_, bl, maybe_corrupt(m.h, corrupt_h_), w, out);
+  assemble_post(hdr_, bl, maybe_corrupt(m.h, corrupt_h_ == 1), w, out);
   auto t2 = std::chrono::steady_clock::now();
   const float vms = verify() ? verify_or_throw(w, out) : 0.f;
   std::lock_guard<std::mutex> lk(tmu_);

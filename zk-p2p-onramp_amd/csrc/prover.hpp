@@ -112,9 +112,13 @@ class Prover {
   // dizkus-scripts/5_gen_proof.sh:14-21): every proof of zkp_prove / zkp_prove_batch /
   // zkp_prove_staged is checked by the host pairing (host_pairing.cpp) against the zkey's
   // verification key; a proof that fails is an error (ZKP_ERR_INTERNAL), never returned.
-  // Default: environment ZKP_VERIFY=1 at load, else off.
-  void set_verify(bool on) { verify_.store(on); }
-  bool verify() const { return verify_.load(); }
+  // Modes: 0 off, 1 every proof, 2 (the default) zkp_prove_batch only -- there the host pairing runs
+  // on the worker thread while the next proof computes (measured free), while on a single proof it
+  // adds its ~2.6 ms to the latency.  Environment ZKP_VERIFY=0/1/2 at load overrides the default.
+  void set_verify(int mode) { verify_.store(mode); }
+  int verify_mode() const { return verify_.load(); }
+  bool verify() const { return verify_.load() == 1; }        // single-proof paths
+  bool verify_batch() const { return verify_.load() != 0; }  // zkp_prove_batch[_status]
 
  private:
   void require_full() const;
@@ -131,8 +135,10 @@ class Prover {
   std::atomic<unsigned> rr_{0};
   mutable std::mutex tmu_;
   float last_ms_[10] = {};  // [8]: verify-before-return (host ms), [9]: witness transfer MB
-  std::atomic<bool> verify_{false};
-  bool corrupt_h_ = false;  // test hook ZKP_TEST_CORRUPT_H=1: piH + G1 generator (a silent device error)
+  std::atomic<int> verify_{2};
+  // test hook ZKP_TEST_CORRUPT_H: 1 = every proof's piH + G1 generator (a silent device error),
+  // 2 = only the odd-indexed proofs of a batch (the batch must refuse those and prove the rest)
+  int corrupt_h_ = 0;
   // throws ZkpError(ZKP_ERR_INTERNAL) unless the assembled proof verifies; returns the host ms spent
   float verify_or_throw(const WtnsView& w, const zkp_proof* out) const;
   friend class DevicePipeline;

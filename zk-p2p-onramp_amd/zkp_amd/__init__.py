@@ -139,9 +139,10 @@ def load_library(path: str = LIB_PATH):
                                                     ctypes.POINTER(u8p), ctypes.POINTER(sz)]
         lib.zkp_blake2b512.argtypes = [u8p, sz, u8p]
         lib.zkp_prover_set_verify.argtypes = [P, ctypes.c_int]
+        lib.zkp_prover_get_verify.argtypes = [P, ctypes.POINTER(ctypes.c_int)]
         lib.zkp_proof_verify.argtypes = [u8p, sz, ctypes.POINTER(_Proof), ctypes.POINTER(ctypes.c_int)]
         lib.zkp_pairing.argtypes = [u8p, u8p, u8p]
-        for name in ("zkp_zkey_beacon_named", "zkp_zkey_contribute_entropy", "zkp_blake2b512", "zkp_prover_set_verify", "zkp_proof_verify", "zkp_pairing", "zkp_prover_load_mem", "zkp_prover_load_file", "zkp_prover_info", "zkp_prove",
+        for name in ("zkp_zkey_beacon_named", "zkp_zkey_contribute_entropy", "zkp_blake2b512", "zkp_prover_set_verify", "zkp_prover_get_verify", "zkp_proof_verify", "zkp_pairing", "zkp_prover_load_mem", "zkp_prover_load_file", "zkp_prover_info", "zkp_prove",
                      "zkp_prove_batch", "zkp_prove_batch_status", "zkp_prove_files", "zkp_proof_json", "zkp_public_json",
                      "zkp_prover_timings", "zkp_msm_g1", "zkp_msm_g2", "zkp_ntt_fr", "zkp_quotient",
                      "zkp_witness_stage", "zkp_prove_staged", "zkp_prover_instrument", "zkp_prover_kernel_stats",
@@ -328,10 +329,20 @@ class Prover:
                 "msm_g1_h", "verify", "wtns_pcie_mb"]
         return dict(zip(keys, list(ms)))
 
-    def set_verify(self, on: bool = True):
-        """Verify-before-return (zkp_prover_set_verify): every proof is checked by the host pairing
-        against the zkey's verification key; a failing proof raises ZkpError (ZKP_ERR_INTERNAL)."""
-        _check(load_library().zkp_prover_set_verify(self._h, 1 if on else 0))
+    VERIFY_OFF, VERIFY_ALL, VERIFY_BATCH = 0, 1, 2
+
+    def set_verify(self, on=True):
+        """Verify-before-return (zkp_prover_set_verify): a checked proof is verified by the host pairing
+        against the zkey's verification key; a failing proof raises ZkpError (ZKP_ERR_INTERNAL), or has
+        that status in a batch.  True / 1: every proof; False / 0: none; 2 (the default at load): the
+        proofs of prove_batch* only."""
+        mode = on if isinstance(on, int) and not isinstance(on, bool) else (1 if on else 0)
+        _check(load_library().zkp_prover_set_verify(self._h, mode))
+
+    def verify_mode(self) -> int:
+        m = ctypes.c_int(-1)
+        _check(load_library().zkp_prover_get_verify(self._h, ctypes.byref(m)))
+        return m.value
 
     def stage(self, wtns: bytes, slot: int, dev_index: int = 0):
         wp, wk = _buf(wtns)
@@ -398,11 +409,13 @@ class Prover:
         lib = load_library()
         n = ctypes.c_int(0)
         _check(lib.zkp_prover_launch_stats(self._h, None, 0, ctypes.byref(n)))
-        out = (ctypes.c_double * (4 * max(1, n.value)))()
-        _check(lib.zkp_prover_launch_stats(self._h, out, n.value, ctypes.byref(n)))
+        cap = n.value
+        out = (ctypes.c_double * (4 * max(1, cap)))()
+        _check(lib.zkp_prover_launch_stats(self._h, out, cap, ctypes.byref(n)))
         v = list(out)
+        # a proof finishing between the two calls grows the record count: read only what fits
         return [{"msm": self.LAUNCH_KINDS[int(v[4 * i])], "adds": int(v[4 * i + 1]), "ms": v[4 * i + 2],
-                 "blocks": int(v[4 * i + 3])} for i in range(n.value)]
+                 "blocks": int(v[4 * i + 3])} for i in range(min(n.value, cap))]
 
     def prove_files(self, wtns_path, proof_path, public_path):
         _check(load_library().zkp_prove_files(self._h, os.fsencode(wtns_path), os.fsencode(proof_path),
