@@ -53,13 +53,29 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+ISSUE_CEILING_TOPS = 256 * 64 * 2.4e9 / 1e12  # one wave64 VALU instruction per SIMD per 4 clocks at 2.4 GHz
+
+
 def load_peak():
-    p = os.path.join(ROOT, "profiles", "ubench_r01.json")
+    """The measured v_mad_u64_u32 peak: profiles/ubench_r05.json (the best row of the occupancy sweep it
+    lists, tools/ubench/int_mul_rate.hip), else round 1's summary."""
+    for name in ("ubench_r05.json", "ubench_r01.json"):
+        p = os.path.join(ROOT, "profiles", name)
+        try:
+            with open(p) as f:
+                return json.load(f)["v_mad_u64_u32_tops"], os.path.relpath(p, ROOT)
+        except Exception:
+            continue
+    return None, None
+
+
+def load_ntt_issue():
+    """Counted NTT issue figures (profiles/ntt_issue_r05.json, the current library: tools/gpu/r5/pmc.sh)."""
     try:
-        with open(p) as f:
-            return json.load(f)["v_mad_u64_u32_tops"], os.path.relpath(p, ROOT)
+        with open(os.path.join(ROOT, "profiles", "ntt_issue_r05.json")) as f:
+            return json.load(f)["sizes"]
     except Exception:
-        return None, None
+        return {}
 
 
 def load_traffic():
@@ -68,6 +84,23 @@ def load_traffic():
     bytes exactly (profiles/fetch_calibration_r02.json; the x2 of coalesced 16-B streams does not
     apply).  Round 4's summary is per launch kind (the H launch, the roofline's); older summaries
     averaged every G1 launch and are recomputed from their raw counters."""
+    p = os.path.join(ROOT, "profiles", "pmc_launch_r05.json")
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        h = d["kinds"]["H"]
+        return {"hbm_bytes_per_launch": h["hbm_bytes_per_dispatch"],
+                "valu_lane_instructions_per_addition": h["valu_lane_instructions_per_addition"],
+                "valu_issue_frac": h["valu_issue_frac"], "clock_GHz": h["clock_GHz"],
+                "per_kind": {k: {"valu_issue_frac_pmc": v["valu_issue_frac"], "clock_GHz_pmc": v["clock_GHz"],
+                                 "valu_lane_instructions_per_addition_pmc": v["valu_lane_instructions_per_addition"],
+                                 "hbm_bytes_per_addition_pmc": v.get("hbm_bytes_per_addition")}
+                             for k, v in d["kinds"].items()},
+                "source": "profiles/pmc_launch_r05.json (the H launch: rocprofv3 --pmc FETCH_SIZE x1 + WRITE_SIZE, "
+                          "gather-calibrated; SQ_INSTS_VALU and GRBM_GUI_ACTIVE: issue share at the launch's own clock; "
+                          "tools/prof/pmc_launch5.py)"}
+    except Exception:
+        pass
     p = os.path.join(ROOT, "profiles", "pmc_launch_r04.json")
     try:
         with open(p) as f:
@@ -169,7 +202,12 @@ def kernel_benches(device, log_n=20, iters=10):
     b20 = min(zkp_amd.bench_ntt(log_n, warmup=3, iters=20, device=device, count=3) for _ in range(3)) / 3
     b23 = min(zkp_amd.bench_ntt(23, warmup=3, iters=20, device=device, count=3) for _ in range(3)) / 3
     return {
+        "msm_kind": "fixed-base: T-row tables 2^(c t) P (t < T) precomputed once per point set, as the prover "
+                    "builds them at zkey load (the Groth16 bases are fixed); their build time is "
+                    "msm_g1_2^20_table_build_ms, outside msm_g1_2^20_ms",
         "msm_g1_2^20_ms": round(st["ms_per_msm"], 3),
+        "msm_g1_2^20_table_build_ms": round(st["table_build_ms"], 3),
+        "msm_g1_2^20_table_rows": st["table_depth"],
         "msm_g1_2^20_result_check": "equal to the c=13/T=1 MSM of the same input",
         "msm_g1_2^20_Mpts_per_s": round(n / st["ms_per_msm"] / 1e3, 1),
         "msm_g1_2^20_accumulate_ms": round(st["ms_accumulate"], 3),
@@ -191,10 +229,18 @@ def ntt_roofline(log_n, ms):
     mac = (2 * (n // 2) * log_n + n) * MAC_PER_FPMUL
     achieved = mac / (ms * 1e-3) / 1e12
     passes = 2 * ((log_n + 7) // 8) - 1
-    return {"bound": "valu-int", "ms": round(ms, 4), "achieved": round(achieved, 3), "peak": peak,
-            "unit": "TMAC/s", "frac": round(achieved / peak, 4) if peak else None,
-            "hbm_pass_GBps": round(passes * 64 * n / (ms * 1e-3) / 1e9, 1),
-            "hbm_frac_of_8TBps": round(passes * 64 * n / (ms * 1e-3) / 8e12, 4)}
+    out = {"bound": "valu-int", "ms": round(ms, 4), "achieved": round(achieved, 3), "peak": peak,
+           "unit": "TMAC/s", "frac": round(achieved / peak, 4) if peak else None,
+           "frac_vs_issue_ceiling": round(achieved / ISSUE_CEILING_TOPS, 4),
+           "hbm_pass_GBps": round(passes * 64 * n / (ms * 1e-3) / 1e9, 1),
+           "hbm_frac_of_8TBps": round(passes * 64 * n / (ms * 1e-3) / 8e12, 4)}
+    cnt = load_ntt_issue().get("2^%d" % log_n, {}).get("cur")
+    if cnt:  # counted on the same library (profiles/ntt_issue_r05.json): per-kernel issue at its own clock
+        out["valu_lane_instr_per_element_pmc"] = cnt["coset_extension_valu_lane_instr_per_element"]
+        out["valu_issue_frac_pmc"] = {k: v["valu_issue_frac"] for k, v in cnt["kernels"].items()}
+        out["clock_GHz_pmc"] = {k: v["clock_GHz"] for k, v in cnt["kernels"].items()}
+        out["pmc_source"] = "profiles/ntt_issue_r05.json"
+    return out
 
 
 S24 = dict(n_vars=16_000_000, n_constraints=(1 << 24) - 27, n_public=26)  # configs[4]
@@ -388,6 +434,13 @@ def accumulate_rooflines(launches, peak, peak_src, traffic):
             lines[k] = line(kinds[k], 1, "k_accumulate<Fq>")
     if "B2" in kinds:
         lines["B2"] = line(kinds["B2"], 3, "k_accumulate<Fq2>")
+    pk = (traffic or {}).get("per_kind", {})
+    for k, ln in lines.items():  # counted issue share and clock of the same kernel (each launch alone)
+        src = pk.get("H" if k == "H" else ("B2" if k == "B2" else "witness (A, B1, C)"))
+        if src:
+            ln.update(src)
+        if ln.get("achieved"):
+            ln["frac_vs_issue_ceiling"] = round(ln["achieved"] / ISSUE_CEILING_TOPS, 4)
     h = lines.get("H") or {}
     roofline = {
         "kernel": "k_accumulate<Fq>, the H MSM launch (G1 bucket accumulation, XYZZ mixed adds)",
@@ -401,6 +454,13 @@ def accumulate_rooflines(launches, peak, peak_src, traffic):
         "algorithmic_work_per_launch": {"mixed_adds": h.get("mixed_adds_per_launch"), "fp_mul_per_add": FPMUL_PER_MADD,
                                         "mac_per_fp_mul": MAC_PER_FPMUL},
         "valu_issue_frac_pmc": traffic.get("valu_issue_frac") if traffic else None,
+        "clock_GHz_pmc": traffic.get("clock_GHz") if traffic else None,
+        "frac_vs_issue_ceiling": round(h["achieved"] / ISSUE_CEILING_TOPS, 4) if h.get("achieved") else None,
+        "issue_ceiling": ISSUE_CEILING_TOPS,
+        "traffic_note": "HBM bytes per launch (FETCH x1 + WRITE): ~101 B per mixed addition, 1.49x the per-addition "
+                        "minimum (64-B base + 4-B index = 68 B) and 13.7x SURVEY.md §8d's MSM floor (2^23 x 96 B): the "
+                        "cost of the 13-row precomputed base table (random gathers over 7 GB; 2.6 L1-TLB misses per "
+                        "addition), at ~1.4 TB/s, 18 % of HBM",
         "valu_lane_instructions_per_addition_pmc": traffic.get("valu_lane_instructions_per_addition") if traffic else None,
         "avg_launch_ms": h.get("avg_launch_ms"),
         "launches_timed": h.get("launches"),

@@ -189,7 +189,8 @@ zkp_status zkp_proof_calldata(const zkp_proof* proof, char* buf, size_t cap, siz
  * [0] wtns H2D, [1] buildABC, [2] NTT/quotient, [3] MSM G1 A,B1,C (own stream, overlaps
  * [1]-[2]), [4] MSM G2 B2 (own stream), [5] host assembly, [6] total wall, [7] MSM G1 H,
  * [8] verify-before-return (host; 0 when off), [9] the witness transfer's PCIe payload in MB
- * (compact encoding; 0 for staged proofs).
+ * (compact encoding; 0 for staged proofs), [10] the witness-MSM configuration
+ * the proof took (0: the default window bits, 1: the second, wider ones; zkp_prover_msm_config).
  * n = capacity of ms (entries beyond n are not written). */
 zkp_status zkp_prover_timings(const zkp_prover* p, float* ms, int n);
 
@@ -283,13 +284,20 @@ zkp_status zkp_prover_kernel_stats(const zkp_prover* p, double* out, int n);
 zkp_status zkp_prover_launch_stats(const zkp_prover* p, double* out, int max_records, int* n_records);
 /* MSM configuration chosen at load (device 0): [0] witness-MSM window bits c, [1] its
  * base-table depth T, [2] its bucket groups ceil(W/T), [3..5] the same for the H MSM,
- * [6] bytes of precomputed base tables per device. */
+ * [6] bytes of precomputed base tables per device, [7..9] c, T and groups of the second witness-MSM
+ * configuration (wider windows, taken by witnesses whose values are mostly >= 2^32; 0 when the
+ * prover keeps only one).  n = capacity of out. */
 zkp_status zkp_prover_msm_config(const zkp_prover* p, double* out, int n);
 /* Device-resident kernel benchmarks.  MSM: stats[0] ms per MSM, [1] ms per
  * accumulate-kernel launch, [2] mixed additions per launch, [3] tasks per launch,
  * [4] window bits c, [5] windows.  out/is_inf receive the result (verification). */
 zkp_status zkp_bench_msm(int device, int g2, const uint8_t* points, const uint8_t* scalars, size_t n, int warmup,
                          int iters, double* stats, uint8_t* out, int* is_inf);
+/* The same with nstats = capacity of stats, and [6] ms to build the base tables (row 0 upload and
+ * conversion + the derived rows 2^(c t) P, t < T: fixed bases, outside the timed MSMs, as the prover
+ * builds them at zkey load), [7] the table depth T (rows per point). */
+zkp_status zkp_bench_msm_ex(int device, int g2, const uint8_t* points, const uint8_t* scalars, size_t n, int warmup,
+                            int iters, double* stats, int nstats, uint8_t* out, int* is_inf);
 /* ms per MSM plan build (digits, bucket grouping, task offsets) of n scalars (32-byte LE):
  * window_bits 0 = automatic; dense != 0: every (window, point) digit an entry, grouped by the
  * hand-written LDS-staged bucket sort (the H MSM's plan), else the compacted witness plan */

@@ -203,9 +203,12 @@ def test_quotient_golden(golden_dir, name):
 # Pippenger parameter variants: window bits c and base-table depth T (T = W: one shared
 # bucket set over precomputed 2^(c t) P rows; T = 1: one bucket group per window;
 # 1 < T < W: several groups folded by Horner with shift c*T).  Bit-exact vs the oracle.
-# (22, 2): 6 groups of 2^21 buckets = 24 key bits, the sort's 6-bit tiled pass C.
+# (22, 2): 6 groups of 2^21 buckets = 24 key bits, the sort's 6-bit tiled pass C; (23, 2): 6 groups of
+# 2^22 buckets = 25 key bits; (24, 1): 11 groups of 2^23 buckets = 27 key bits, the largest the sort
+# takes (b3 = 9).
 @pytest.mark.parametrize("dense", ["1", "0"])
-@pytest.mark.parametrize("c,depth", [(0, 1), (8, 0), (8, 3), (9, 7), (13, 0), (20, 0), (24, 0), (22, 2)])
+@pytest.mark.parametrize("c,depth", [(0, 1), (8, 0), (8, 3), (9, 7), (13, 0), (20, 0), (24, 0), (22, 2), (23, 2),
+                                     (24, 1)])
 def test_msm_g1_params(monkeypatch, c, depth, dense):
     _plan(monkeypatch, dense)
     pts = _pts(200, 5)

@@ -121,3 +121,28 @@ def test_batch_of_mixes_on_inflight_pipelines(setup, monkeypatch):
         p.close()
     for i, (g, (_, want)) in enumerate(zip(got, cases)):
         assert g[0] == want, (i, kinds[i])
+
+
+@pytest.mark.parametrize("kind", ["bits", "all_large"])
+@pytest.mark.parametrize("wsel", ["first", "second", "auto"])
+def test_witness_configurations_equal_oracle(setup, kind, wsel, monkeypatch):
+    """Both resident witness-MSM configurations (window bits c and c + 2, prover.hip pick_wset): a
+    proof equals oracle/cpu's whichever one it takes -- forced first or second, or chosen per proof by
+    the witness's share of values >= 2^32 (auto: the uniform witness takes the second, the 0/1-heavy
+    one the first), from a host witness and from a staged one."""
+    monkeypatch.setenv("ZKP_MSM", "wsel=%s" % wsel)
+    w, want = _case(setup, kind)
+    p = zkp_amd.Prover(setup[1], devices=[0])
+    try:
+        cfg = p.msm_config()
+        assert cfg["witness_second"] and cfg["witness_second"]["c"] == cfg["witness"]["c"] + 2
+        got, _ = p.prove_raw(w, R_FIX, S_FIX)
+        took = p.timings()["witness_config"]
+        p.stage(w, slot=0)
+        staged, _ = p.prove_staged_raw(0, R_FIX, S_FIX)
+        took_staged = p.timings()["witness_config"]
+    finally:
+        p.close()
+    assert got == want and staged == want
+    expect = {"first": 0, "second": 1, "auto": 1 if kind == "all_large" else 0}[wsel]
+    assert took == expect and took_staged == expect

@@ -591,15 +591,21 @@ zkp_status zkp_prover_launch_stats(const zkp_prover* p, double* out, int max_rec
   return guard([&] { *n_records = p->impl->launch_records(out, max_records); });
 }
 
-zkp_status zkp_bench_msm(int device, int g2, const uint8_t* points, const uint8_t* scalars, size_t n, int warmup,
-                         int iters, double* stats, uint8_t* out, int* is_inf) {
-  if (!points || !scalars || !stats) return fail(ZKP_ERR_INVALID_ARG, "null argument");
+zkp_status zkp_bench_msm_ex(int device, int g2, const uint8_t* points, const uint8_t* scalars, size_t n, int warmup,
+                            int iters, double* stats, int nstats, uint8_t* out, int* is_inf) {
+  if (!points || !scalars || !stats || nstats < 0) return fail(ZKP_ERR_INVALID_ARG, "null argument");
   return guard([&] {
     zkp::MsmBench b = zkp::bench_msm(device, g2 ? zkp::Curve::G2 : zkp::Curve::G1, points, scalars, n, warmup,
                                      iters, out, is_inf);
-    stats[0] = b.ms_per_msm, stats[1] = b.ms_accumulate, stats[2] = (double)b.mixed_adds;
-    stats[3] = (double)b.tasks, stats[4] = b.c, stats[5] = b.windows;
+    const double v[8] = {b.ms_per_msm, b.ms_accumulate, (double)b.mixed_adds, (double)b.tasks,
+                         (double)b.c, (double)b.windows, (double)b.table_ms, (double)b.depth};
+    for (int i = 0; i < nstats && i < 8; ++i) stats[i] = v[i];
   });
+}
+
+zkp_status zkp_bench_msm(int device, int g2, const uint8_t* points, const uint8_t* scalars, size_t n, int warmup,
+                         int iters, double* stats, uint8_t* out, int* is_inf) {
+  return zkp_bench_msm_ex(device, g2, points, scalars, n, warmup, iters, stats, 6, out, is_inf);
 }
 
 zkp_status zkp_bench_plan(int device, const uint8_t* scalars, size_t n, int window_bits, int dense, int warmup,

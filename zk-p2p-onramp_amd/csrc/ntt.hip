@@ -236,6 +236,36 @@ __device__ __forceinline__ int brev_src(const Tile& T, int e) {
   return (e & ~mask) | (int)(brev(k1, T.b) << T.lc);
 }
 
+// Addresses of element e = threadIdx.x + it * NTT_TPB of a full tile.  tile_coords (global index,
+// position in its block), the LDS slot swz(e) and the digit-reversed slot swz(brev_src(e)) are all
+// linear in e's bit-fields (disjoint bits add, resp. XOR), so each is the part of threadIdx.x --
+// computed once per thread (lane_base) -- plus the part of it * NTT_TPB, the same for every lane
+// (scalar registers; lane_at): ~2 vector instructions per element and phase instead of ~15 (round 5)
+struct Lane {
+  size_t g;
+  uint32_t pos;
+  int sw, sb;  // swz(e), swz(brev_src(e))
+};
+__device__ __forceinline__ Lane lane_base(const Tile& T, uint32_t tile) {
+  Lane L;
+  tile_coords(T, tile, (int)threadIdx.x, L.g, L.pos);
+  L.sw = swz((int)threadIdx.x);
+  L.sb = swz(brev_src(T, (int)threadIdx.x));
+  return L;
+}
+__device__ __forceinline__ Lane lane_at(const Lane& L, const Tile& T, uint32_t tile, int it) {
+  size_t gz, gh;
+  uint32_t pz, ph;
+  tile_coords(T, tile, 0, gz, pz);
+  tile_coords(T, tile, it * NTT_TPB, gh, ph);
+  Lane r;
+  r.g = L.g + (gh - gz);
+  r.pos = L.pos + (ph - pz);
+  r.sw = L.sw ^ swz(it * NTT_TPB);
+  r.sb = L.sb ^ swz(brev_src(T, it * NTT_TPB));
+  return r;
+}
+
 // MODE 0: DIF pass (DFT, then inter-pass twiddle), 1: DIT pass (twiddle, then DFT),
 // 2: the fused innermost pair of coset_extend (lm == b): inverse-root DFT, coset key
 //    (table by digit-reversed position), forward-root DFT on one LDS-resident tile.
@@ -252,23 +282,29 @@ __global__ __launch_bounds__(NTT_TPB) void k_ntt(Polys P, Tile T, const uint32_t
   uint32_t* __restrict__ data = vec == 0 ? P.p0 : (vec == 1 ? P.p1 : P.p2);
   stage_roots(ltw, rootsA);
   constexpr int VPT = (1 << LOG_TILE) / NTT_TPB;  // elements per thread of a full tile
+  Lane L0{};
+  if (LE) L0 = lane_base(T, tile);
   if (LE && MODE == 1 && tw) {
     // full tiles: the twiddle products of two elements at a time in lockstep (mul_pair)
 #pragma unroll
     for (int it = 0; it < VPT; it += 2) {
-      const int e0 = (int)threadIdx.x + it * NTT_TPB, e1 = e0 + NTT_TPB;
-      size_t g0, g1;
-      uint32_t pos0, pos1;
-      tile_coords(T, tile, e0, g0, pos0);
-      tile_coords(T, tile, e1, g1, pos1);
+      const Lane a = lane_at(L0, T, tile, it), c = lane_at(L0, T, tile, it + 1);
       Fr x0, x1;
-      mul_pair(load_fe<FrCfg>(data + g0 * 8), load_fe<FrCfg>(tw + (size_t)pos0 * 8), load_fe<FrCfg>(data + g1 * 8),
-               load_fe<FrCfg>(tw + (size_t)pos1 * 8), x0, x1);
+      mul_pair(load_fe<FrCfg>(data + a.g * 8), load_fe<FrCfg>(tw + (size_t)a.pos * 8), load_fe<FrCfg>(data + c.g * 8),
+               load_fe<FrCfg>(tw + (size_t)c.pos * 8), x0, x1);
 #pragma unroll
       for (int l = 0; l < NL; ++l) {
-        lds[l * E + swz(e0)] = x0.v[l];
-        lds[l * E + swz(e1)] = x1.v[l];
+        lds[l * E + a.sw] = x0.v[l];
+        lds[l * E + c.sw] = x1.v[l];
       }
+    }
+  } else if (LE) {
+#pragma unroll
+    for (int it = 0; it < VPT; ++it) {
+      const Lane a = lane_at(L0, T, tile, it);
+      const Fr x = load_fe<FrCfg>(data + a.g * 8);
+#pragma unroll
+      for (int l = 0; l < NL; ++l) lds[l * E + a.sw] = x.v[l];
     }
   } else {
     for (int e = threadIdx.x; e < E; e += NTT_TPB) {
@@ -293,19 +329,14 @@ __global__ __launch_bounds__(NTT_TPB) void k_ntt(Polys P, Tile T, const uint32_t
     if (LE) {
 #pragma unroll
       for (int it = 0; it < VPT; it += 2) {
-        const int e0 = (int)threadIdx.x + it * NTT_TPB, e1 = e0 + NTT_TPB;
-        const int src0 = swz(brev_src(T, e0)), src1 = swz(brev_src(T, e1));
+        const Lane a = lane_at(L0, T, tile, it), c = lane_at(L0, T, tile, it + 1);
         Fr x0, x1;
 #pragma unroll
         for (int l = 0; l < NL; ++l) {
-          x0.v[l] = lds[l * E + src0];
-          x1.v[l] = lds[l * E + src1];
+          x0.v[l] = lds[l * E + a.sb];
+          x1.v[l] = lds[l * E + c.sb];
         }
-        size_t g0, g1;
-        uint32_t pos0, pos1;
-        tile_coords(T, tile, e0, g0, pos0);
-        tile_coords(T, tile, e1, g1, pos1);
-        mul_pair(x0, load_fe<FrCfg>(coset + g0 * 8), x1, load_fe<FrCfg>(coset + g1 * 8), v[it], v[it + 1]);
+        mul_pair(x0, load_fe<FrCfg>(coset + a.g * 8), x1, load_fe<FrCfg>(coset + c.g * 8), v[it], v[it + 1]);
       }
     } else {
 #pragma unroll
@@ -329,8 +360,9 @@ __global__ __launch_bounds__(NTT_TPB) void k_ntt(Polys P, Tile T, const uint32_t
     for (int it = 0; it < VPT; ++it) {
       const int e = (int)threadIdx.x + it * NTT_TPB;
       if (e < E) {
+        const int sw = LE ? lane_at(L0, T, tile, it).sw : swz(e);
 #pragma unroll
-        for (int l = 0; l < NL; ++l) lds[l * E + swz(e)] = v[it].v[l];
+        for (int l = 0; l < NL; ++l) lds[l * E + sw] = v[it].v[l];
       }
     }
     __syncthreads();
@@ -339,22 +371,27 @@ __global__ __launch_bounds__(NTT_TPB) void k_ntt(Polys P, Tile T, const uint32_t
   if (LE && MODE == 0 && tw) {
 #pragma unroll
     for (int it = 0; it < VPT; it += 2) {
-      const int e0 = (int)threadIdx.x + it * NTT_TPB, e1 = e0 + NTT_TPB;
-      const int src0 = swz(brev_src(T, e0)), src1 = swz(brev_src(T, e1));
+      const Lane a = lane_at(L0, T, tile, it), c = lane_at(L0, T, tile, it + 1);
       Fr x0, x1;
 #pragma unroll
       for (int l = 0; l < NL; ++l) {
-        x0.v[l] = lds[l * E + src0];
-        x1.v[l] = lds[l * E + src1];
+        x0.v[l] = lds[l * E + a.sb];
+        x1.v[l] = lds[l * E + c.sb];
       }
-      size_t g0, g1;
-      uint32_t pos0, pos1;
-      tile_coords(T, tile, e0, g0, pos0);
-      tile_coords(T, tile, e1, g1, pos1);
       Fr y0, y1;
-      mul_pair(x0, load_fe<FrCfg>(tw + (size_t)pos0 * 8), x1, load_fe<FrCfg>(tw + (size_t)pos1 * 8), y0, y1);
-      store_fe(data + g0 * 8, y0);
-      store_fe(data + g1 * 8, y1);
+      mul_pair(x0, load_fe<FrCfg>(tw + (size_t)a.pos * 8), x1, load_fe<FrCfg>(tw + (size_t)c.pos * 8), y0, y1);
+      store_fe(data + a.g * 8, y0);
+      store_fe(data + c.g * 8, y1);
+    }
+  } else if (LE) {
+#pragma unroll
+    for (int it = 0; it < VPT; ++it) {
+      const Lane a = lane_at(L0, T, tile, it);
+      Fr x;
+#pragma unroll
+      for (int l = 0; l < NL; ++l) x.v[l] = lds[l * E + a.sb];
+      if (MODE == 0 && tw) x = mul(x, load_fe<FrCfg>(tw + (size_t)a.pos * 8));
+      store_fe(data + a.g * 8, x);
     }
   } else {
     for (int e = threadIdx.x; e < E; e += NTT_TPB) {

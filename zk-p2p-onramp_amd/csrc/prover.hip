@@ -113,9 +113,14 @@ static int env_int(const char* name, int dflt) {
 //   seg=<n>               buckets per bucket-reduction segment (a power of two; default 4)
 //   plan=dense|compact    the plan variant of the kernel-level MSMs (zkp_msm_*; default dense)
 // A malformed value or an unknown key is a ZKP_ERR_INVALID_ARG: a typo never silently tunes nothing.
+//   w2=<bits>             window bits of the second witness plan (default w + 2; full provers only)
+//   wsets=1|2             witness-MSM configurations kept resident (default 2: w and w2)
+//   wsel=first|second|auto  which one a proof takes (default auto: by the witness's share of values
+//                         >= 2^32, DevicePipeline::pick_wset)
 struct MsmOptions {
-  int w = 0, h = 0, depth = 0, task_w = 0, task_h = 0, seg = 0;
+  int w = 0, h = 0, depth = 0, task_w = 0, task_h = 0, seg = 0, w2 = 0, wsets = 2;
   int dense = 1;
+  int wsel = 0;  // 0 auto, 1 first, 2 second
 };
 static MsmOptions msm_options() {
   MsmOptions o;
@@ -137,14 +142,22 @@ static MsmOptions msm_options() {
       o.dense = val == "dense" ? 1 : 0;
       continue;
     }
+    if (key == "wsel") {
+      if (val != "first" && val != "second" && val != "auto")
+        throw ZkpError(ZKP_ERR_INVALID_ARG, "ZKP_MSM: wsel=first|second|auto");
+      o.wsel = val == "first" ? 1 : (val == "second" ? 2 : 0);
+      continue;
+    }
     char* stop = nullptr;
     const long v = std::strtol(val.c_str(), &stop, 10);
     if (val.empty() || *stop || v <= 0 || v > (1 << 20))
       throw ZkpError(ZKP_ERR_INVALID_ARG, "ZKP_MSM: bad value in '" + item + "'");
     int* dst = key == "w" ? &o.w : key == "h" ? &o.h : key == "depth" ? &o.depth : key == "task_w" ? &o.task_w
-             : key == "task_h" ? &o.task_h : key == "seg" ? &o.seg : nullptr;
+             : key == "task_h" ? &o.task_h : key == "seg" ? &o.seg : key == "w2" ? &o.w2
+             : key == "wsets" ? &o.wsets : nullptr;
     if (!dst) throw ZkpError(ZKP_ERR_INVALID_ARG, "ZKP_MSM: unknown key '" + key + "'");
     if (key == "seg" && (v & (v - 1))) throw ZkpError(ZKP_ERR_INVALID_ARG, "ZKP_MSM: seg must be a power of two");
+    if (key == "wsets" && v > 2) throw ZkpError(ZKP_ERR_INVALID_ARG, "ZKP_MSM: wsets=1|2");
     *dst = (int)v;
   }
   return o;
@@ -303,31 +316,58 @@ class DevicePipeline {
     split_range(h.n_vars, part, nparts, wlo_, whi_);
     split_range(h.domain_size, part, nparts, hlo_, hhi_);
     const size_t nv = whi_ - wlo_, nd = hhi_ - hlo_;
+    const MsmOptions opt = msm_options();
     MsmParams pw, ph;
-    choose_msm_params(nv, nd, msm_options(), pw, ph);
+    choose_msm_params(nv, nd, opt, pw, ph);
+    wsel_opt_ = opt.wsel;
     // base tables: A, B1, C, B2 indexed by witness signal (C's first nPublic+1 bases are
     // infinity, so one witness plan serves all four), H by domain index
+    auto build_wtables = [&](WSet& w) {
+      w.ta = std::make_shared<MsmBases>(Curve::G1, nv, w.pw.c, w.pw.depth);
+      w.tb1 = std::make_shared<MsmBases>(Curve::G1, nv, w.pw.c, w.pw.depth);
+      w.tc = std::make_shared<MsmBases>(Curve::G1, nv, w.pw.c, w.pw.depth);
+      w.tb2 = std::make_shared<MsmBases>(Curve::G2, nv, w.pw.c, w.pw.depth);
+      fill_bases(*w.ta, z.bf.sec[5].ptr + wlo_ * 64, nv, 0, s0_);
+      fill_bases(*w.tb1, z.bf.sec[6].ptr + wlo_ * 64, nv, 0, s0_);
+      fill_bases(*w.tb2, z.bf.sec[7].ptr + wlo_ * 128, nv, 0, s0_);
+      const size_t cfirst = std::max(wlo_, c0);  // first witness index of the slice with a C base
+      const size_t lead = std::min(cfirst, whi_) - wlo_;
+      const size_t cnt = whi_ > cfirst ? whi_ - cfirst : 0;
+      fill_bases(*w.tc, cnt ? z.bf.sec[8].ptr + (cfirst - c0) * 64 : nullptr, cnt, lead, s0_);
+    };
     if (share) {
       if (share->dev_ != dev_ || share->wlo_ != wlo_ || share->whi_ != whi_ || share->hlo_ != hlo_ ||
           share->hhi_ != hhi_)
         throw ZkpError(ZKP_ERR_INTERNAL, "shared base tables of another device or slice");
-      ta_ = share->ta_, tb1_ = share->tb1_, tc_ = share->tc_, tb2_ = share->tb2_, th_ = share->th_;
-    } else {
-      ta_ = std::make_shared<MsmBases>(Curve::G1, nv, pw.c, pw.depth);
-      tb1_ = std::make_shared<MsmBases>(Curve::G1, nv, pw.c, pw.depth);
-      tc_ = std::make_shared<MsmBases>(Curve::G1, nv, pw.c, pw.depth);
-      tb2_ = std::make_shared<MsmBases>(Curve::G2, nv, pw.c, pw.depth);
-      th_ = std::make_shared<MsmBases>(Curve::G1, nd, ph.c, ph.depth);
-      fill_bases(*ta_, z.bf.sec[5].ptr + wlo_ * 64, nv, 0, s0_);
-      fill_bases(*tb1_, z.bf.sec[6].ptr + wlo_ * 64, nv, 0, s0_);
-      fill_bases(*tb2_, z.bf.sec[7].ptr + wlo_ * 128, nv, 0, s0_);
-      {
-        const size_t cfirst = std::max(wlo_, c0);  // first witness index of the slice with a C base
-        const size_t lead = std::min(cfirst, whi_) - wlo_;
-        const size_t cnt = whi_ > cfirst ? whi_ - cfirst : 0;
-        fill_bases(*tc_, cnt ? z.bf.sec[8].ptr + (cfirst - c0) * 64 : nullptr, cnt, lead, s0_);
+      nws_ = share->nws_;
+      for (int k = 0; k < nws_; ++k) {
+        const WSet& o = share->ws_[k];
+        ws_[k].pw = o.pw, ws_[k].ta = o.ta, ws_[k].tb1 = o.tb1, ws_[k].tc = o.tc, ws_[k].tb2 = o.tb2;
       }
+      th_ = share->th_;
+    } else {
+      ws_[0].pw = pw;
+      build_wtables(ws_[0]);
+      th_ = std::make_shared<MsmBases>(Curve::G1, nd, ph.c, ph.depth);
       fill_bases(*th_, z.bf.sec[9].ptr + hlo_ * 64, nd, 0, s0_);
+      // the second witness configuration (round 5): c = w + 2 bits, one bucket set,
+      // for witnesses whose values are mostly >= 2^32 (all-uniform: c = 20 is ~7 % faster than 18 on the
+      // Venmo shape, profiles/wsweep_r04.txt); full provers only, and only where its tables fit in half
+      // of the HBM still free (the Venmo key: +26.6 GB)
+      const int c2 = opt.w2 ? opt.w2 : std::min(24, pw.c + 2);
+      if (nparts == 1 && opt.wsets == 2 && c2 != pw.c) {
+        HIPX(hipStreamSynchronize(s0_));
+        size_t free_b = 0, total_b = 0;
+        HIPX(hipMemGetInfo(&free_b, &total_b));
+        const MsmParams p2 = make_params(nv, c2, 0);
+        if ((size_t)p2.windows * nv * (3 * 64 + 128) <= free_b / 2) {
+          ws_[1].pw = make_params(nv, c2, p2.windows);
+          if (opt.task_w > 0) ws_[1].pw.S = opt.task_w;
+          if (opt.seg > 0 && opt.seg <= (1 << (ws_[1].pw.c - 1))) ws_[1].pw.M = opt.seg;
+          build_wtables(ws_[1]);
+          nws_ = 2;
+        }
+      }
     }
     for (int m = 0; m < 2; ++m) {
       const Csr& c = z.csr[m];
@@ -343,21 +383,8 @@ class DevicePipeline {
     }
     // witness upload slots: each has its own copy stream, so a proof's
     // witness H2D runs outside the compute lock and overlaps the proof in flight, and its own pinned
-    // staging buffer and copy threads (upload())
-    {
-      const size_t stage_words = std::max<size_t>(wt_chunks(h.n_vars), 1) * wt_chunk_words();
-      for (int k = 0; k < NUP; ++k) {
-        HIPX(hipMalloc(&up_[k], std::max<size_t>((size_t)h.n_vars * 32, 32)));
-        HIPX(hipMalloc(&upstage_[k], stage_words * 4));
-        HIPX(hipHostMalloc(&uph_[k], stage_words * 4, hipHostMallocDefault));
-        HIPX(hipStreamCreateWithFlags(&sup_[k], hipStreamNonBlocking));
-        for (int j = 0; j + 1 < NDMA; ++j) {
-          HIPX(hipStreamCreateWithFlags(&sdma_[k][j], hipStreamNonBlocking));
-          HIPX(hipEventCreateWithFlags(&evdma_[k][j], hipEventDisableTiming));
-        }
-        for (auto& t : copiers_[k]) t = std::make_unique<JobThread>();
-      }
-    }
+    // staging buffer and copy threads (upload()); allocated on the slot's first host-witness upload
+    // (ensure_upload_slot), so staged-only and split provers hold no pinned staging or copy threads
     for (auto& b : abc_) HIPX(hipMalloc(&b, nd_all * 32));
     HIPX(hipMalloc(&pscal_, nd_all * 32));
     ntt_ = std::make_unique<NttEngine>((int)h.log_domain, s0_);
@@ -365,16 +392,19 @@ class DevicePipeline {
     // plans and runs the H MSM.  The witness plan runs on the high-priority finish stream s3 (ahead
     // of its G1 finishes), so its sort passes are not starved by the quotient's NTTs on s0: the
     // witness accumulations start ~5 ms earlier; proof 26.69 -> 26.58 ms (profiles/wplan_r03.txt)
-    plan_w_ = std::make_unique<MsmPlan>(nv, pw, s3_);
+    for (int k = 0; k < nws_; ++k) {
+      WSet& w = ws_[k];
+      w.plan = std::make_unique<MsmPlan>(nv, w.pw, s3_);
+      for (auto& g : w.g1) g = std::make_unique<MsmEngine>(Curve::G1, w.pw, nv, s2_);
+      w.g2 = std::make_unique<MsmEngine>(Curve::G2, w.pw, nv, s1_);
+      wina_ = std::max(wina_, w.g1[0]->window_words());
+      win2_ = std::max(win2_, w.g2->window_words());
+    }
     plan_h_ = std::make_unique<MsmPlan>(nd, ph, s0_);
     // H scalars are uniform (quotient evaluations): dense plan (one workgroup per sub-bin)
     plan_h_->set_dense(true);
-    for (auto& g : g1w_) g = std::make_unique<MsmEngine>(Curve::G1, pw, nv, s2_);
-    g2_ = std::make_unique<MsmEngine>(Curve::G2, pw, nv, s1_);
     g1h_ = std::make_unique<MsmEngine>(Curve::G1, ph, nd, s0_);
-    wina_ = g1w_[0]->window_words();
     winh_ = g1h_->window_words();
-    win2_ = g2_->window_words();
     HIPX(hipMalloc(&dwin_, win_total() * 4));
     HIPX(hipHostMalloc(&hwin_, win_total() * 4, hipHostMallocDefault));
     HIPX(hipStreamSynchronize(s0_));
@@ -383,15 +413,9 @@ class DevicePipeline {
   ~DevicePipeline() {
     (void)hipSetDevice(dev_);
     ntt_.reset();
-    for (auto& g : g1w_) g.reset();
+    for (auto& w : ws_) w = WSet{};
     g1h_.reset();
-    g2_.reset();
-    plan_w_.reset();
     plan_h_.reset();
-    ta_.reset();
-    tb1_.reset();
-    tc_.reset();
-    tb2_.reset();
     th_.reset();
     for (void* p : {(void*)rowptr_[0], (void*)rowptr_[1], (void*)col_[0], (void*)col_[1], (void*)val_[0],
                     (void*)val_[1], (void*)up_[0], (void*)up_[1], (void*)abc_[0], (void*)abc_[1], (void*)abc_[2],
@@ -423,6 +447,7 @@ class DevicePipeline {
     Jac<HFq2> b2;
     float ms[6];
     float pcie_mb = 0;  // witness transfer payload (prove() from a host witness)
+    int wset = 0;       // the witness configuration the proof took (pick_wset)
   };
   // called with a, b1, c, b2 folded (h not yet) while the H MSM still runs on the device
   using EarlyFn = std::function<void(const MsmOut&)>;
@@ -467,9 +492,26 @@ class DevicePipeline {
   // is encoded, so encoding and PCIe overlap; one kernel then expands the chunks into the 32-B
   // witness layout.  A 0/1-heavy witness moves ~2.5x fewer bytes; an all-uniform one as many plus the
   // meta.  Returns the wall time (ms).
+  // the resources of upload slot k, created on its first use (the caller holds slot k)
+  void ensure_upload_slot(int k) {
+    if (up_[k]) return;
+    const size_t stage_words = std::max<size_t>(wt_chunks(hdr_.n_vars), 1) * wt_chunk_words();
+    // (each piece only if missing: a failed first attempt leaves no leak behind the next one)
+    if (!upstage_[k]) HIPX(hipMalloc(&upstage_[k], stage_words * 4));
+    if (!uph_[k]) HIPX(hipHostMalloc(&uph_[k], stage_words * 4, hipHostMallocDefault));
+    if (!sup_[k]) HIPX(hipStreamCreateWithFlags(&sup_[k], hipStreamNonBlocking));
+    for (int j = 0; j + 1 < NDMA; ++j) {
+      if (!sdma_[k][j]) HIPX(hipStreamCreateWithFlags(&sdma_[k][j], hipStreamNonBlocking));
+      if (!evdma_[k][j]) HIPX(hipEventCreateWithFlags(&evdma_[k][j], hipEventDisableTiming));
+    }
+    for (auto& t : copiers_[k])
+      if (!t) t = std::make_unique<JobThread>();
+    HIPX(hipMalloc(&up_[k], std::max<size_t>((size_t)hdr_.n_vars * 32, 32)));  // last: marks the slot ready
+  }
   float upload(int k, const WtnsView& w, uint64_t* pcie_bytes = nullptr) {
     HIPX(hipSetDevice(dev_));
     const auto t0 = std::chrono::steady_clock::now();
+    ensure_upload_slot(k);
     const uint32_t n = hdr_.n_vars;
     const uint32_t nch = wt_chunks(n);
     const size_t chw = wt_chunk_words();
@@ -478,6 +520,7 @@ class DevicePipeline {
     hipStream_t st = sup_[k];
     std::exception_ptr errs[NCOPY];
     std::atomic<uint64_t> sent{0};
+    std::atomic<uint32_t> large{0};
     constexpr int T = NCOPY;
     // chunk c's DMA goes to stream c % NDMA: one copy queue serialises the ~100 chunk copies with
     // ~10 us between them (rocprofv3 --memory-copy-trace: 2.7 ms for 62 MB), parallel queues overlap
@@ -486,12 +529,14 @@ class DevicePipeline {
     auto part = [&](int t) {
       try {
         HIPX(hipSetDevice(dev_));
+        uint32_t nl = 0;
         for (uint32_t c = (uint32_t)t; c < nch; c += (uint32_t)T) {
-          const size_t words = wt_encode_chunk(src, n, c, pin + (size_t)c * chw);
+          const size_t words = wt_encode_chunk(src, n, c, pin + (size_t)c * chw, &nl);
           HIPX(hipMemcpyAsync(upstage_[k] + (size_t)c * chw, pin + (size_t)c * chw, words * 4, hipMemcpyHostToDevice,
                               dma_stream(c)));
           sent += words * 4;
         }
+        large += nl;
       } catch (...) {
         errs[t] = std::current_exception();
       }
@@ -514,6 +559,7 @@ class DevicePipeline {
     launch_witness_unpack(upstage_[k], 0, n, up_[k], st);
     HIPX(hipStreamSynchronize(st));
     if (pcie_bytes) *pcie_bytes = sent.load();
+    up_large_[k] = n ? (double)large.load() / n : 0.0;
     return std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
   }
   MsmOut prove_uploaded(int k, float h2d_ms, const EarlyFn& early = {}) {
@@ -522,7 +568,7 @@ class DevicePipeline {
     maybe_inject_fault();
     HIPX(hipEventRecord(ev_[0], s0_));
     HIPX(hipEventRecord(ev_[1], s0_));
-    MsmOut o = prove_dev(up_[k], early);
+    MsmOut o = prove_dev(up_[k], early, pick_wset(up_large_[k]));
     o.ms[0] = h2d_ms;
     return o;
   }
@@ -559,8 +605,23 @@ class DevicePipeline {
     if (slot < 0 || slot > 4096) throw ZkpError(ZKP_ERR_INVALID_ARG, "bad staging slot");
     if ((size_t)slot >= slots_.size()) slots_.resize(slot + 1, nullptr);
     if (!slots_[slot]) HIPX(hipMalloc(&slots_[slot], (size_t)hdr_.n_vars * 32));
+    if ((size_t)slot >= slot_large_.size()) slot_large_.resize(slot + 1, 0.0);
     HIPX(hipMemcpyAsync(slots_[slot], w.values, (size_t)hdr_.n_vars * 32, hipMemcpyHostToDevice, s0_));
+    // the share of values >= 2^32 (pick_wset), counted while the copy runs
+    size_t nl = 0;
+    for (size_t i = 0; i < hdr_.n_vars; ++i) {
+      const uint8_t* v = w.values + 32 * i;
+      uint32_t w1;
+      uint64_t hi[3];
+      std::memcpy(&w1, v + 4, 4);
+      std::memcpy(hi, v + 8, 24);
+      nl += (w1 | hi[0] | hi[1] | hi[2]) != 0;
+    }
+    slot_large_[slot] = hdr_.n_vars ? (double)nl / hdr_.n_vars : 0.0;
     HIPX(hipStreamSynchronize(s0_));
+  }
+  double slot_large(int slot) const {  // caller holds the staging lock (shared)
+    return slot >= 0 && (size_t)slot < slot_large_.size() ? slot_large_[slot] : 0.0;
   }
   const uint32_t* slot_ptr(int slot) const {
     if (slot < 0 || (size_t)slot >= slots_.size() || !slots_[slot])
@@ -570,9 +631,11 @@ class DevicePipeline {
 
   void set_instrument(bool on) {
     std::lock_guard<std::mutex> lk(mu_);
-    for (auto& g : g1w_) g->set_instrument(on);
+    for (int k = 0; k < nws_; ++k) {
+      for (auto& g : ws_[k].g1) g->set_instrument(on);
+      ws_[k].g2->set_instrument(on);
+    }
     g1h_->set_instrument(on);
-    g2_->set_instrument(on);
     stats_g1_ = MsmEngine::Stats{};
     stats_g2_ = MsmEngine::Stats{};
     launches_.clear();
@@ -588,13 +651,26 @@ class DevicePipeline {
     std::lock_guard<std::mutex> lk(mu_);
     out.insert(out.end(), launches_.begin(), launches_.end());
   }
-  void msm_params(MsmParams& pw, MsmParams& ph) const {
-    pw = plan_w_->params();
+  void msm_params(MsmParams& pw, MsmParams& ph, MsmParams* pw2 = nullptr) const {
+    pw = ws_[0].plan->params();
     ph = plan_h_->params();
+    if (pw2) *pw2 = nws_ > 1 ? ws_[1].plan->params() : MsmParams{};
   }
+  int witness_sets() const { return nws_; }
   size_t table_bytes() const {
-    return ta_->bytes() + tb1_->bytes() + tc_->bytes() + tb2_->bytes() + th_->bytes();
+    size_t b = th_->bytes();
+    for (int k = 0; k < nws_; ++k) b += ws_[k].ta->bytes() + ws_[k].tb1->bytes() + ws_[k].tc->bytes() + ws_[k].tb2->bytes();
+    return b;
   }
+  // the witness configuration a proof takes: the second (wider windows) when the witness's share of
+  // values >= 2^32 is above WSET2_LARGE_FRAC (each such value carries a digit in every window; 0/1 and
+  // other small values only one or two), unless ZKP_MSM wsel= fixes it
+  int pick_wset(double large_frac) const {
+    if (nws_ < 2 || wsel_opt_ == 1) return 0;
+    if (wsel_opt_ == 2) return 1;
+    return large_frac > WSET2_LARGE_FRAC ? 1 : 0;
+  }
+  static constexpr double WSET2_LARGE_FRAC = 0.55;
 
   void quotient(const WtnsView& w, uint8_t* out) {
     UploadSlot slot(this);
@@ -665,26 +741,29 @@ class DevicePipeline {
 
   MsmOut prove_staged(int slot, const EarlyFn& early = {}) {
     std::shared_lock<std::shared_mutex> sl(stage_mu_);
-    return prove_resident(slot_ptr(slot), early);
+    return prove_resident(slot_ptr(slot), early, slot_large(slot));
   }
   // shared hold of this (first) pipeline's staging slots for a proof that reads one of them
   std::shared_lock<std::shared_mutex> hold_stage() { return std::shared_lock<std::shared_mutex>(stage_mu_); }
 
   // a proof of a witness already resident on this GPU: this pipeline's staging slot, or a
   // ZKP_INFLIGHT sibling's (staged witnesses live in the device's first pipeline)
-  MsmOut prove_resident(const uint32_t* d_wit, const EarlyFn& early = {}) {
+  MsmOut prove_resident(const uint32_t* d_wit, const EarlyFn& early = {}, double large_frac = 0.0) {
     std::lock_guard<std::mutex> lk(mu_);
     HIPX(hipSetDevice(dev_));
     HIPX(hipEventRecord(ev_[0], s0_));
     HIPX(hipEventRecord(ev_[1], s0_));
-    return prove_dev(d_wit, early);
+    return prove_dev(d_wit, early, pick_wset(large_frac));
   }
   // claimed by a staged caller (Prover::prove_staged spreads concurrent callers over the pipelines)
   std::atomic<bool> staged_busy{false};
 
   // the whole device pipeline on a resident witness (caller holds mu_, ev_[0..1] recorded)
-  MsmOut prove_dev(const uint32_t* d_wit, const EarlyFn& early = {}) {
-    // group-sum layout in dwin_: A | B1 | C (engines g1w_) | H (g1h) | B2 (g2)
+  MsmOut prove_dev(const uint32_t* d_wit, const EarlyFn& early = {}, int wsel = 0) {
+    WSet& ws = ws_[wsel < nws_ ? wsel : 0];
+    const size_t win2 = ws.g2->window_words();
+    // group-sum layout in dwin_ (slots sized for the larger witness configuration): A | B1 | C
+    // (engines ws.g1) | H (g1h) | B2 (ws.g2)
     uint32_t* wa = dwin_;
     uint32_t* wh = dwin_ + 3 * wina_;
     uint32_t* wb2 = wh + winh_;
@@ -705,16 +784,16 @@ class DevicePipeline {
         HIPX(hipSetDevice(dev_));
         HIPX(hipStreamWaitEvent(s2_, ev_[1], 0));
         HIPX(hipEventRecord(ev_[9], s2_));
-        HIPX(hipStreamWaitEvent(plan_w_->stream(), ev_[1], 0));
-        plan_w_->build(d_wit + wlo_ * 8, whi_ - wlo_);
+        HIPX(hipStreamWaitEvent(ws.plan->stream(), ev_[1], 0));
+        ws.plan->build(d_wit + wlo_ * 8, whi_ - wlo_);
         planned.set_value();
         planned_set = true;
-        const MsmBases* tabs[3] = {ta_.get(), tb1_.get(), tc_.get()};
+        const MsmBases* tabs[3] = {ws.ta.get(), ws.tb1.get(), ws.tc.get()};
         for (int m = 0; m < 3; ++m) {
-          g1w_[m]->accumulate(*plan_w_, *tabs[m]);
+          ws.g1[m]->accumulate(*ws.plan, *tabs[m]);
           HIPX(hipEventRecord(ev_[10 + m], s2_));
           HIPX(hipStreamWaitEvent(s3_, ev_[10 + m], 0));
-          g1w_[m]->finish(*plan_w_, wa + m * wina_, s3_);
+          ws.g1[m]->finish(*ws.plan, wa + m * wina_, s3_);
           if (serial_) {  // profiling: no overlap between the finish and the next accumulation
             HIPX(hipEventRecord(ev_[13], s3_));
             HIPX(hipStreamWaitEvent(s2_, ev_[13], 0));
@@ -734,8 +813,8 @@ class DevicePipeline {
         HIPX(hipEventRecord(ev_[7], s1_));
         // the finish on s1 too: s3 is in-order, the G1 finishes must not queue behind it (gating the
         // G2 finish on the H plan, on either stream, measured +0.9 ms: profiles/g2_finish_r03.txt)
-        g2_->accumulate(*plan_w_, *tb2_);
-        g2_->finish(*plan_w_, wb2, s1_);
+        ws.g2->accumulate(*ws.plan, *ws.tb2);
+        ws.g2->finish(*ws.plan, wb2, s1_);
         HIPX(hipEventRecord(ev_[6], s1_));
       } catch (...) {
         err[1] = std::current_exception();
@@ -780,13 +859,12 @@ class DevicePipeline {
     // affine conversions and the H fold remain after the device is done
     HIPX(hipStreamWaitEvent(s3_, ev_[6], 0));
     HIPX(hipMemcpyAsync(hwin_, dwin_, 3 * wina_ * 4, hipMemcpyDeviceToHost, s3_));
-    HIPX(hipMemcpyAsync(hwin_ + 3 * wina_ + winh_, wb2, (win_total() - 3 * wina_ - winh_) * 4, hipMemcpyDeviceToHost,
-                        s3_));
+    HIPX(hipMemcpyAsync(hwin_ + 3 * wina_ + winh_, wb2, win2 * 4, hipMemcpyDeviceToHost, s3_));
     HIPX(hipEventRecord(ev_[15], s3_));
     HIPX(hipMemcpyAsync(hwin_ + 3 * wina_, wh, winh_ * 4, hipMemcpyDeviceToHost, s0_));
     HIPX(hipEventRecord(ev_[5], s0_));
     MsmOut o;
-    const MsmParams& pa = g1w_[0]->params();
+    const MsmParams& pa = ws.g1[0]->params();
     const MsmParams& ph = g1h_->params();
     HIPX(hipEventSynchronize(ev_[15]));
     o.a = msm_fold<HFq>(hwin_, pa);
@@ -804,9 +882,10 @@ class DevicePipeline {
     }
     HIPX(hipStreamSynchronize(s0_));
     HIPX(hipStreamSynchronize(s3_));
-    for (int m = 0; m < 3; ++m) collect_kind(*g1w_[m], m, stats_g1_);
+    for (int m = 0; m < 3; ++m) collect_kind(*ws.g1[m], m, stats_g1_);
     collect_kind(*g1h_, 3, stats_g1_);
-    collect_kind(*g2_, 4, stats_g2_);
+    collect_kind(*ws.g2, 4, stats_g2_);
+    o.wset = wsel < nws_ ? wsel : 0;
     o.h = msm_fold<HFq>(hwin_ + 3 * wina_, ph);
     HIPX(hipEventElapsedTime(&o.ms[0], ev_[0], ev_[1]));  // wtns H2D
     HIPX(hipEventElapsedTime(&o.ms[1], ev_[1], ev_[2]));  // buildABC
@@ -825,7 +904,17 @@ class DevicePipeline {
   hipStream_t s0_ = nullptr, s1_ = nullptr, s2_ = nullptr, s3_ = nullptr;
   hipEvent_t ev_[16];
   JobThread jt_g1_, jt_g2_;  // host threads feeding s2 (witness plan, G1 MSMs) and s1 (G2 MSM)
-  std::shared_ptr<MsmBases> ta_, tb1_, tc_, tb2_, th_;  // shared by the pipelines of one device
+  // one witness-MSM configuration (the witness plan serves A, B1, C and B2): window bits, base tables
+  // (shared by the pipelines of one device), plan and engines (per pipeline)
+  struct WSet {
+    MsmParams pw;
+    std::shared_ptr<MsmBases> ta, tb1, tc, tb2;
+    std::unique_ptr<MsmPlan> plan;
+    std::unique_ptr<MsmEngine> g1[3], g2;  // g1: A, B1, C
+  };
+  WSet ws_[2];
+  int nws_ = 1, wsel_opt_ = 0;
+  std::shared_ptr<MsmBases> th_;  // shared by the pipelines of one device
   uint32_t* rowptr_[2] = {nullptr, nullptr};
   uint32_t* col_[2] = {nullptr, nullptr};
   uint32_t* val_[2] = {nullptr, nullptr};
@@ -855,15 +944,17 @@ class DevicePipeline {
   uint32_t* pscal_ = nullptr;
   const uint32_t* ext_abc_[3] = {nullptr, nullptr, nullptr};  // set only inside prove_ext_staged
   std::unique_ptr<NttEngine> ntt_;
-  std::unique_ptr<MsmPlan> plan_w_, plan_h_;
-  std::unique_ptr<MsmEngine> g1w_[3], g1h_, g2_;  // g1w_: A, B1, C
-  size_t wina_ = 0, winh_ = 0, win2_ = 0;
+  std::unique_ptr<MsmPlan> plan_h_;
+  std::unique_ptr<MsmEngine> g1h_;
+  size_t wina_ = 0, winh_ = 0, win2_ = 0;  // group-sum slot sizes (max over the witness configurations)
   size_t win_total() const { return 3 * wina_ + winh_ + win2_; }
   uint32_t* dwin_ = nullptr;
   uint32_t* hwin_ = nullptr;
   std::mutex mu_;
   std::shared_mutex stage_mu_;  // staging slots (see stage())
   std::vector<uint32_t*> slots_;
+  std::vector<double> slot_large_;     // per staging slot: share of witness values >= 2^32
+  double up_large_[NUP] = {0.0, 0.0};  // per upload slot, of the witness last uploaded
   MsmEngine::Stats stats_g1_, stats_g2_;
   std::vector<std::array<double, 4>> launches_;  // {kind, adds, ms, workgroups} per instrumented launch (capped)
   void collect_kind(MsmEngine& e, int kind, MsmEngine::Stats& agg) {
@@ -1109,6 +1200,7 @@ void Prover::prove_partial(const uint8_t* wtns, size_t len, zkp_partial* out) {
   for (int i = 0; i < 5; ++i) last_ms_[i] = m.ms[i];
   last_ms_[7] = m.ms[5];
   last_ms_[9] = m.pcie_mb;
+  last_ms_[10] = (float)m.wset;
 }
 
 void Prover::prove_partial_staged(int slot, zkp_partial* out) {
@@ -1118,6 +1210,7 @@ void Prover::prove_partial_staged(int slot, zkp_partial* out) {
   for (int i = 0; i < 5; ++i) last_ms_[i] = m.ms[i];
   last_ms_[7] = m.ms[5];
   last_ms_[9] = m.pcie_mb;
+  last_ms_[10] = (float)m.wset;
 }
 
 void Prover::quotient_part_staged(int slot, int mask, void* const* dst) {
@@ -1132,6 +1225,7 @@ void Prover::prove_partial_ext_staged(int slot, const void* const* abc, zkp_part
   for (int i = 0; i < 5; ++i) last_ms_[i] = m.ms[i];
   last_ms_[7] = m.ms[5];
   last_ms_[9] = m.pcie_mb;
+  last_ms_[10] = (float)m.wset;
 }
 
 void proof_combine(const uint8_t* zkey, size_t len, const zkp_partial* parts, int nparts, const uint8_t* wtns,
@@ -1177,6 +1271,7 @@ void Prover::prove(const uint8_t* wtns, size_t len, const uint8_t* r32, const ui
   for (int i = 0; i < 5; ++i) last_ms_[i] = m.ms[i];
   last_ms_[7] = m.ms[5];
   last_ms_[9] = m.pcie_mb;
+  last_ms_[10] = (float)m.wset;
   last_ms_[5] = std::chrono::duration<float, std::milli>(t2 - t1).count();
   last_ms_[6] = std::chrono::duration<float, std::milli>(t2 - t0).count();
   last_ms_[8] = vms;
@@ -1291,7 +1386,7 @@ void Prover::quotient(const uint8_t* wtns, size_t len, uint8_t* out) {
 
 void Prover::timings(float* ms, int n) const {
   std::lock_guard<std::mutex> lk(tmu_);
-  for (int i = 0; i < n && i < 10; ++i) ms[i] = last_ms_[i];
+  for (int i = 0; i < n && i < 11; ++i) ms[i] = last_ms_[i];
 }
 
 DevicePipeline& Prover::staged_pipeline(int dev_index) const {
@@ -1318,6 +1413,7 @@ void Prover::prove_staged(int dev, int slot, const uint8_t* r32, const uint8_t* 
   DevicePipeline& base = staged_pipeline(dev);
   auto staged = base.hold_stage();  // the slot stays valid and unchanged until the proof is done
   const uint32_t* d_wit = base.slot_ptr(slot);
+  const double large_frac = base.slot_large(slot);
   // concurrent staged callers on one device take its idle ZKP_INFLIGHT pipelines (the staged
   // witnesses live in the first one; the others read them in place); with none idle the call
   // queues on the first pipeline
@@ -1338,7 +1434,7 @@ void Prover::prove_staged(int dev, int slot, const uint8_t* r32, const uint8_t* 
   auto t0 = std::chrono::steady_clock::now();
   Blinded bl;
   DevicePipeline::MsmOut m = d->prove_resident(
-      d_wit, [&](const DevicePipeline::MsmOut& o) { bl = assemble_pre(hdr_, o, r32, s32); });
+      d_wit, [&](const DevicePipeline::MsmOut& o) { bl = assemble_pre(hdr_, o, r32, s32); }, large_frac);
   auto t1 = std::chrono::steady_clock::now();
   WtnsView w;
   {
@@ -1353,6 +1449,7 @@ void Prover::prove_staged(int dev, int slot, const uint8_t* r32, const uint8_t* 
   for (int i = 0; i < 5; ++i) last_ms_[i] = m.ms[i];
   last_ms_[7] = m.ms[5];
   last_ms_[9] = m.pcie_mb;
+  last_ms_[10] = (float)m.wset;
   last_ms_[5] = std::chrono::duration<float, std::milli>(t2 - t1).count();
   last_ms_[6] = std::chrono::duration<float, std::milli>(t2 - t0).count();
   last_ms_[8] = vms;
@@ -1363,11 +1460,13 @@ void Prover::set_instrument(bool on) {
 }
 
 void Prover::msm_config(double* out, int n) const {
-  MsmParams pw, ph;
-  devs_[0]->msm_params(pw, ph);
-  const double v[7] = {(double)pw.c, (double)pw.depth, (double)pw.groups, (double)ph.c,
-                       (double)ph.depth, (double)ph.groups, (double)devs_[0]->table_bytes()};
-  for (int i = 0; i < n && i < 7; ++i) out[i] = v[i];
+  MsmParams pw, ph, pw2;
+  devs_[0]->msm_params(pw, ph, &pw2);
+  const bool two = devs_[0]->witness_sets() > 1;
+  const double v[10] = {(double)pw.c, (double)pw.depth, (double)pw.groups, (double)ph.c,
+                        (double)ph.depth, (double)ph.groups, (double)devs_[0]->table_bytes(),
+                        two ? (double)pw2.c : 0.0, two ? (double)pw2.depth : 0.0, two ? (double)pw2.groups : 0.0};
+  for (int i = 0; i < n && i < 10; ++i) out[i] = v[i];
 }
 
 void Prover::kernel_stats(double* out, int n) const {
@@ -1405,6 +1504,7 @@ struct MsmRig {
   uint32_t *ds = nullptr, *dw = nullptr;
   size_t n;
   Curve curve;
+  float table_ms = 0;  // base-table build: row 0 upload + conversion + the derived rows (HIP events)
   MsmRig(int device, Curve cv, const uint8_t* points, const uint8_t* scalars, size_t n_, int c, int depth)
       : n(n_), curve(cv) {
     HIPX(hipSetDevice(device));
@@ -1420,7 +1520,15 @@ struct MsmRig {
       const int c_auto = dense_window_bits(std::min(20, std::max(8, lg - 3)), n);
       prm = make_params(std::max<size_t>(n, 1), c ? c : c_auto, depth);
       bases = std::make_unique<MsmBases>(curve, n, prm.c, prm.depth);
+      hipEvent_t t0, t1;
+      HIPX(hipEventCreate(&t0));
+      HIPX(hipEventCreate(&t1));
+      HIPX(hipEventRecord(t0, st));
       fill_bases(*bases, points, n, 0, st);
+      HIPX(hipEventRecord(t1, st));
+      HIPX(hipEventSynchronize(t1));
+      HIPX(hipEventElapsedTime(&table_ms, t0, t1));
+      (void)hipEventDestroy(t0), (void)hipEventDestroy(t1);
       plan = std::make_unique<MsmPlan>(std::max<size_t>(n, 1), prm, st);
       plan->set_dense(opt.dense != 0);
       eng = std::make_unique<MsmEngine>(curve, prm, std::max<size_t>(n, 1), st);
@@ -1512,6 +1620,8 @@ MsmBench bench_msm(int device, Curve curve, const uint8_t* points, const uint8_t
     r.tasks = s.tasks / std::max<uint64_t>(1, s.launches);
     r.c = rig.prm.c;
     r.windows = rig.prm.windows;
+    r.depth = rig.prm.depth;
+    r.table_ms = rig.table_ms;
     if (out && is_inf) rig.result(out, is_inf);
   } catch (...) {
     (void)hipEventDestroy(e0), (void)hipEventDestroy(e1);

@@ -106,7 +106,8 @@ class Prover {
   int part() const { return part_; }
   int nparts() const { return nparts_; }
   // MSM configuration of device 0: [0] witness c, [1] witness depth, [2] witness groups,
-  // [3] H c, [4] H depth, [5] H groups, [6] base-table bytes per device
+  // [3] H c, [4] H depth, [5] H groups, [6] base-table bytes per device, [7..9] the second witness
+  // configuration's c, depth, groups (0 when the prover keeps one)
   void msm_config(double* out, int n) const;
   // verify-before-return (the reference verifies every proof after proving,
   // dizkus-scripts/5_gen_proof.sh:14-21): every proof of zkp_prove / zkp_prove_batch /
@@ -134,7 +135,7 @@ class Prover {
   mutable std::mutex smu_;
   std::atomic<unsigned> rr_{0};
   mutable std::mutex tmu_;
-  float last_ms_[10] = {};  // [8]: verify-before-return (host ms), [9]: witness transfer MB
+  float last_ms_[11] = {};  // [8]: verify-before-return (host ms), [9]: witness transfer MB, [10]: witness MSM configuration
   std::atomic<int> verify_{2};
   // test hook ZKP_TEST_CORRUPT_H: 1 = every proof's piH + G1 generator (a silent device error),
   // 2 = only the odd-indexed proofs of a batch (the batch must refuse those and prove the rest)
@@ -167,6 +168,8 @@ struct MsmBench {
   uint64_t mixed_adds = 0;      // per launch
   uint64_t tasks = 0;           // per launch
   int c = 0, windows = 0;
+  int depth = 0;        // base-table rows T (T = windows: every window's 2^(c t) P precomputed)
+  float table_ms = 0;   // building those tables (outside the timed MSMs: fixed bases, built at load)
 };
 MsmBench bench_msm(int device, Curve curve, const uint8_t* points, const uint8_t* scalars, size_t n, int warmup,
                    int iters, uint8_t* out, int* is_inf);

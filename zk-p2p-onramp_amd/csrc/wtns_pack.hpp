@@ -29,13 +29,15 @@ inline uint32_t wt_chunks(uint32_t n) { return (wt_blocks(n) + WT_CHUNK_BLOCKS -
 
 // encodes chunk c of the n-signal witness at src into its region (wt_chunk_words() words); returns
 // the number of leading words of the region to send.  Every store lands inside the block's own
-// payload (no stray writes; the slack words are kept as a guard).
-inline size_t wt_encode_chunk(const uint8_t* src, uint32_t n, uint32_t c, uint32_t* region) {
+// payload (no stray writes; the slack words are kept as a guard).  n_large (optional): incremented by
+// the chunk's count of values >= 2^32 (the prover picks its witness MSM configuration from it).
+inline size_t wt_encode_chunk(const uint8_t* src, uint32_t n, uint32_t c, uint32_t* region,
+                              uint32_t* n_large = nullptr) {
   const uint32_t nblk = wt_blocks(n);
   const uint32_t b0 = c * WT_CHUNK_BLOCKS, b1 = nblk < b0 + WT_CHUNK_BLOCKS ? nblk : b0 + WT_CHUNK_BLOCKS;
   uint32_t* meta = region;
   uint32_t* pay = region + WT_META_WORDS;
-  uint32_t off = 0;
+  uint32_t off = 0, nl = 0;
   for (uint32_t b = b0; b < b1; ++b) {
     const uint32_t i0 = b * WT_BLOCK, m = n - i0 < WT_BLOCK ? n - i0 : WT_BLOCK;
     const uint8_t* v = src + (size_t)i0 * 32;
@@ -80,7 +82,9 @@ inline size_t wt_encode_chunk(const uint8_t* src, uint32_t n, uint32_t c, uint32
     mb[5] = (uint32_t)(bitv >> 32);
     mb[6] = off;
     off += (8 * L + ns + 3) & ~3u;
+    nl += L;
   }
+  if (n_large) *n_large += nl;
   _mm_sfence();  // the non-temporal stores are globally visible before the chunk's DMA is enqueued
   return WT_META_WORDS + off;
 }

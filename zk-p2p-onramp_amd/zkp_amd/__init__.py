@@ -104,6 +104,10 @@ def load_library(path: str = LIB_PATH):
                                                 ctypes.POINTER(ctypes.c_int)]
         lib.zkp_bench_msm.argtypes = [ctypes.c_int, ctypes.c_int, u8p, u8p, sz, ctypes.c_int, ctypes.c_int,
                                       ctypes.POINTER(ctypes.c_double), u8p, ctypes.POINTER(ctypes.c_int)]
+        if hasattr(lib, "zkp_bench_msm_ex"):
+            lib.zkp_bench_msm_ex.argtypes = [ctypes.c_int, ctypes.c_int, u8p, u8p, sz, ctypes.c_int, ctypes.c_int,
+                                             ctypes.POINTER(ctypes.c_double), ctypes.c_int, u8p,
+                                             ctypes.POINTER(ctypes.c_int)]
         lib.zkp_bench_ntt.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                       ctypes.POINTER(ctypes.c_double)]
         lib.zkp_bench_ntt_batch.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
@@ -139,7 +143,8 @@ def load_library(path: str = LIB_PATH):
                                                     ctypes.POINTER(u8p), ctypes.POINTER(sz)]
         lib.zkp_blake2b512.argtypes = [u8p, sz, u8p]
         lib.zkp_prover_set_verify.argtypes = [P, ctypes.c_int]
-        lib.zkp_prover_get_verify.argtypes = [P, ctypes.POINTER(ctypes.c_int)]
+        if hasattr(lib, "zkp_prover_get_verify"):  # round-5 entry points (an older library loads for A/B runs)
+            lib.zkp_prover_get_verify.argtypes = [P, ctypes.POINTER(ctypes.c_int)]
         lib.zkp_proof_verify.argtypes = [u8p, sz, ctypes.POINTER(_Proof), ctypes.POINTER(ctypes.c_int)]
         lib.zkp_pairing.argtypes = [u8p, u8p, u8p]
         for name in ("zkp_zkey_beacon_named", "zkp_zkey_contribute_entropy", "zkp_blake2b512", "zkp_prover_set_verify", "zkp_prover_get_verify", "zkp_proof_verify", "zkp_pairing", "zkp_prover_load_mem", "zkp_prover_load_file", "zkp_prover_info", "zkp_prove",
@@ -147,12 +152,13 @@ def load_library(path: str = LIB_PATH):
                      "zkp_prover_timings", "zkp_msm_g1", "zkp_msm_g2", "zkp_ntt_fr", "zkp_quotient",
                      "zkp_witness_stage", "zkp_prove_staged", "zkp_prover_instrument", "zkp_prover_kernel_stats",
                      "zkp_prover_launch_stats",
-                     "zkp_bench_msm", "zkp_bench_ntt", "zkp_bench_ntt_batch", "zkp_bench_plan", "zkp_msm", "zkp_prover_msm_config",
+                     "zkp_bench_msm", "zkp_bench_msm_ex", "zkp_bench_ntt", "zkp_bench_ntt_batch", "zkp_bench_plan", "zkp_msm", "zkp_prover_msm_config",
                      "zkp_prover_load_part", "zkp_prove_partial", "zkp_proof_calldata",
                      "zkp_prover_load_chunks", "zkp_zkey_read", "zkp_zkey_read_chunks", "zkp_zkey_contribute", "zkp_zkey_new",
                      "zkp_beacon_secret", "zkp_zkey_beacon", "zkp_prove_partial_staged", "zkp_proof_combine",
                      "zkp_quotient_part_staged", "zkp_prove_partial_ext_staged"):
-            getattr(lib, name).restype = ctypes.c_int
+            if hasattr(lib, name):
+                getattr(lib, name).restype = ctypes.c_int
         _lib = lib
         return lib
 
@@ -323,10 +329,10 @@ class Prover:
 
     def timings(self):
         lib = load_library()
-        ms = (ctypes.c_float * 10)()
-        _check(lib.zkp_prover_timings(self._h, ms, 10))
+        ms = (ctypes.c_float * 11)()
+        _check(lib.zkp_prover_timings(self._h, ms, 11))
         keys = ["wtns_h2d", "build_abc", "ntt_quotient", "msm_g1_abc", "msm_g2", "host_assembly", "total_wall",
-                "msm_g1_h", "verify", "wtns_pcie_mb"]
+                "msm_g1_h", "verify", "wtns_pcie_mb", "witness_config"]
         return dict(zip(keys, list(ms)))
 
     VERIFY_OFF, VERIFY_ALL, VERIFY_BATCH = 0, 1, 2
@@ -387,12 +393,13 @@ class Prover:
         return out.raw
 
     def msm_config(self):
-        out = (ctypes.c_double * 7)()
-        _check(load_library().zkp_prover_msm_config(self._h, out, 7))
+        out = (ctypes.c_double * 10)()
+        _check(load_library().zkp_prover_msm_config(self._h, out, 10))
         v = list(out)
         return {"witness": {"c": int(v[0]), "depth": int(v[1]), "groups": int(v[2])},
                 "h": {"c": int(v[3]), "depth": int(v[4]), "groups": int(v[5])},
-                "table_bytes_per_device": int(v[6])}
+                "table_bytes_per_device": int(v[6]),
+                "witness_second": ({"c": int(v[7]), "depth": int(v[8]), "groups": int(v[9])} if v[7] else None)}
 
     def kernel_stats(self):
         out = (ctypes.c_double * 8)()
@@ -748,11 +755,11 @@ def bench_msm(points_lem: bytes, scalars_le: bytes, g2: bool = False, warmup: in
     n = len(scalars_le) // 32
     pp, pk = _buf(points_lem)
     sp, sk = _buf(scalars_le)
-    st = (ctypes.c_double * 6)()
+    st = (ctypes.c_double * 8)()
     out = (ctypes.c_uint8 * 128)()
     inf = ctypes.c_int()
-    _check(lib.zkp_bench_msm(device, 1 if g2 else 0, pp, sp, n, warmup, iters, st,
-                             ctypes.cast(out, ctypes.POINTER(ctypes.c_uint8)), ctypes.byref(inf)))
+    _check(lib.zkp_bench_msm_ex(device, 1 if g2 else 0, pp, sp, n, warmup, iters, st, 8,
+                                ctypes.cast(out, ctypes.POINTER(ctypes.c_uint8)), ctypes.byref(inf)))
     raw = bytes(out)
     if inf.value:
         res = None
@@ -762,7 +769,7 @@ def bench_msm(points_lem: bytes, scalars_le: bytes, g2: bool = False, warmup: in
     else:
         res = (_le(raw[:32]), _le(raw[32:64]))
     stats = {"ms_per_msm": st[0], "ms_accumulate": st[1], "mixed_adds": int(st[2]), "tasks": int(st[3]),
-             "c": int(st[4]), "windows": int(st[5])}
+             "c": int(st[4]), "windows": int(st[5]), "table_build_ms": st[6], "table_depth": int(st[7])}
     return stats, res
 
 
