@@ -171,7 +171,9 @@ zkp_status zkp_proof_combine(const uint8_t* zkey, size_t len, const zkp_partial*
                              zkp_proof* out);
 
 /* CLI-equivalent: `groth16 prove <zkey> <wtns> <proof.json> <public.json>` on a
- * loaded prover; writes JSON byte-compatible with snarkjs (JSON.stringify(x,null,1)). */
+ * loaded prover; writes JSON byte-compatible with snarkjs (JSON.stringify(x,null,1)).
+ * A regular witness file is memory-mapped for the transfer: it must not be truncated by another
+ * writer during the call (other file kinds are read into a buffer first). */
 zkp_status zkp_prove_files(zkp_prover* p, const char* wtns_path, const char* proof_json_path,
                            const char* public_json_path);
 

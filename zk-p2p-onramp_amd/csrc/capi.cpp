@@ -76,14 +76,17 @@ std::vector<uint8_t> read_file(const char* path) {
 
 // A witness file mapped read-only: the prover's transfer threads read the page cache directly (the
 // page faults spread over them) instead of one thread copying 205 MB into a zero-filled buffer
-// first.  Falls back to read_file() where the file cannot be mapped.
+// first.  Regular files only; anything else (a pipe, a device, a procfs node) and a file that cannot
+// be mapped is read into a buffer (read_file).  A mapped file must not be truncated by another writer
+// while the call runs (the read of a page past the new end would raise SIGBUS): include/zkp_amd.h
+// states this for zkp_prove_files.
 class MappedFile {
  public:
   explicit MappedFile(const char* path) {
     const int fd = ::open(path, O_RDONLY | O_CLOEXEC);
     if (fd < 0) throw zkp::ZkpError(ZKP_ERR_IO, std::string("cannot open ") + path);
     struct stat st {};
-    if (::fstat(fd, &st) == 0 && st.st_size > 0) {
+    if (::fstat(fd, &st) == 0 && S_ISREG(st.st_mode) && st.st_size > 0) {
       void* m = ::mmap(nullptr, (size_t)st.st_size, PROT_READ, MAP_PRIVATE, fd, 0);
       if (m != MAP_FAILED) {
         map_ = m;
