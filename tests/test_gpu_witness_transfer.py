@@ -115,6 +115,9 @@ def test_batch_of_mixes_on_inflight_pipelines(setup, monkeypatch):
     kinds = ["all_large", "natural", "edges", "bits", "all_small", "natural", "all_large", "edges"]
     cases = [_case(setup, k) for k in kinds]
     p = zkp_amd.Prover(setup[1], devices=[0])
+    # these witnesses do not satisfy the circuit (module docstring): the batch's default
+    # verify-before-return would refuse their proofs, so it is off here
+    p.set_verify(False)
     try:
         got = p.prove_batch_raw([w for w, _ in cases], rs=[R_FIX] * len(cases), ss=[S_FIX] * len(cases))
     finally:
