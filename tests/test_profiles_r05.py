@@ -61,3 +61,30 @@ def test_ubench_peak_is_best_sweep_row():
     u = json.load(open(os.path.join(P, "ubench_r05.json")))
     assert u["v_mad_u64_u32_tops"] == max(r["tops"] for r in u["sweep"])
     assert len(u["sweep"]) == 15 and abs(u["issue_ceiling_tops"] - 256 * 64 * 2.4e9 / 1e12) < 1e-3
+
+
+def test_launch_split_r05_reproduces_bench_fracs(tmp_path):
+    """The round-5 kernel trace (k_accumulate rows + the ROCTx "bench timed" range of the same bench
+    invocation) recomputes every launch kind's frac of profiles/bench_r05_rocprof_run.json within 0.01."""
+    out = tmp_path / "split.json"
+    subprocess.run([sys.executable, os.path.join(ROOT, "tools", "prof", "launch_split.py"),
+                    os.path.join(P, "rocprof_r05_accumulate_trace.csv"), os.path.join(P, "rocprof_r05_marker_trace.csv"),
+                    os.path.join(P, "bench_r05_rocprof_run.json"), str(out)], check=True, capture_output=True, timeout=120)
+    res = json.loads(out.read_text())
+    assert set(res["kinds"]) == {"A", "B1", "C", "H", "B2"}
+    for kind, v in res["kinds"].items():
+        assert v["dispatches"] == v["bench_launches"], kind
+        assert abs(v["frac_delta"]) <= 0.01, (kind, v)
+    bench = json.loads(open(os.path.join(P, "bench_r05_rocprof_run.json")).read())
+    assert bench["roofline"]["valu_issue_frac_pmc"] is not None and bench["roofline"]["clock_GHz_pmc"] is not None
+
+
+def test_host_capacity_covers_eight_gpus():
+    """profiles/host_capacity_r05.json: 8 concurrent encoder groups on the GPU box's
+    16-core quota keep up with 8 GPUs' worth of proofs for both witness mixes."""
+    d = json.load(open(os.path.join(P, "host_capacity_r05.json")))
+    best = {}
+    for r in d["host_capacity"]:
+        if r["groups"] == 8:
+            best[r["bool_pct"]] = max(best.get(r["bool_pct"], 0), r["witnesses_per_s"])
+    assert best[70] > 2 * 320 and best[0] > 2 * 160

@@ -233,8 +233,10 @@ void MsmBases::extend(hipStream_t st) {
 
 // ------------------------------------------------------------------ MsmPlan
 
-MsmPlan::MsmPlan(size_t max_n, const MsmParams& prm, hipStream_t stream)
-    : prm_(prm), max_n_(std::max<size_t>(max_n, 1)), stream_(stream) {
+MsmPlan::MsmPlan(Init, size_t max_n, const MsmParams& prm, hipStream_t stream)
+    : prm_(prm), max_n_(std::max<size_t>(max_n, 1)), stream_(stream) {}
+
+MsmPlan::MsmPlan(size_t max_n, const MsmParams& prm, hipStream_t stream) : MsmPlan(Init{}, max_n, prm, stream) {
   if (prm_.c < MsmParams::MIN_C || prm_.c > MsmParams::MAX_C || prm_.windows > HS_STAGE / HS_TPB)
     throw std::invalid_argument("MSM: window bits outside the plan's range");
   if (max_n_ * prm_.depth >= (size_t(1) << 31)) throw std::runtime_error("MSM size too large for 31-bit base indices");
@@ -400,8 +402,11 @@ void MsmPlan::build(const uint32_t* scalars, size_t n) {
 
 // ------------------------------------------------------------------ MsmEngine
 
+MsmEngine::MsmEngine(Init, Curve curve, const MsmParams& prm, size_t max_n, hipStream_t stream)
+    : curve_(curve), prm_(prm), max_n_(std::max<size_t>(max_n, 1)), stream_(stream) {}
+
 MsmEngine::MsmEngine(Curve curve, const MsmParams& prm, size_t max_n, hipStream_t stream)
-    : curve_(curve), prm_(prm), max_n_(std::max<size_t>(max_n, 1)), stream_(stream) {
+    : MsmEngine(Init{}, curve, prm, max_n, stream) {
   fwords_ = curve_fwords(curve);
   const size_t half = prm_.half();
   nbuckets_ = prm_.buckets();
@@ -426,8 +431,8 @@ MsmEngine::MsmEngine(Curve curve, const MsmParams& prm, size_t max_n, hipStream_
 
 MsmEngine::~MsmEngine() {
   for (auto& e : ev_) {
-    (void)hipEventDestroy(e[0]);
-    (void)hipEventDestroy(e[1]);
+    if (e[0]) (void)hipEventDestroy(e[0]);
+    if (e[1]) (void)hipEventDestroy(e[1]);
   }
   if (h_counts_) (void)hipHostFree(h_counts_);
   for (void* p : {(void*)part_a_, (void*)part_b_, (void*)buckets_, (void*)seg_s_, (void*)seg_t_, (void*)sub_[0],

@@ -131,6 +131,10 @@ class MsmBases {
 };
 
 class MsmPlan {
+  struct Init {};  // the delegated-to constructor: members only, so a failing allocation in the
+                   // delegating one runs the destructor (no device memory leaks on out-of-memory)
+  MsmPlan(Init, size_t max_n, const MsmParams& prm, hipStream_t stream);
+
  public:
   MsmPlan(size_t max_n, const MsmParams& prm, hipStream_t stream);
   ~MsmPlan();
@@ -195,6 +199,9 @@ class MsmPlan {
 };
 
 class MsmEngine {
+  struct Init {};  // as MsmPlan::Init
+  MsmEngine(Init, Curve curve, const MsmParams& prm, size_t max_n, hipStream_t stream);
+
  public:
   MsmEngine(Curve curve, const MsmParams& prm, size_t max_n, hipStream_t stream);
   ~MsmEngine();
@@ -247,7 +254,7 @@ class MsmEngine {
   static constexpr int MAX_PENDING = 16;
   bool instrument_ = false;
   int pending_ = 0;
-  hipEvent_t ev_[MAX_PENDING][2];
+  hipEvent_t ev_[MAX_PENDING][2] = {};
   uint32_t* h_counts_ = nullptr;  // pinned: tasks per pending run, then entries per pending run
   uint32_t h_total_[MAX_PENDING] = {};
   bool h_total_dev_[MAX_PENDING] = {};

@@ -3,6 +3,7 @@
 
 #include <functional>
 
+#include <sched.h>
 #include <sys/random.h>
 
 #include <algorithm>
@@ -98,6 +99,27 @@ static U256 scalar_or_random(const uint8_t* s32) {
 static void put_fq(const HFq& x, uint8_t* out) { host::u256_to_le(x.to_std(), out); }
 
 // ------------------------------------------------------------------ device pipeline
+
+// host cores this process may use: the affinity mask, capped by a cgroup v2 CPU quota (the GPU boxes
+// show 256 CPUs to nproc but allow 16)
+static int host_cores() {
+  static const int n = [] {
+    int c = (int)std::thread::hardware_concurrency();
+    cpu_set_t set;
+    if (sched_getaffinity(0, sizeof(set), &set) == 0) c = CPU_COUNT(&set);
+    if (FILE* f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {
+      char q[32] = {0};
+      long per = 0;
+      if (std::fscanf(f, "%31s %ld", q, &per) == 2 && std::strcmp(q, "max") != 0 && per > 0) {
+        const long quota = std::atol(q);
+        if (quota > 0) c = std::min(c, (int)std::max(1L, (quota + per / 2) / per));
+      }
+      std::fclose(f);
+    }
+    return std::max(1, c);
+  }();
+  return n;
+}
 
 static int env_int(const char* name, int dflt) {
   const char* v = std::getenv(name);
@@ -392,19 +414,36 @@ class DevicePipeline {
     // plans and runs the H MSM.  The witness plan runs on the high-priority finish stream s3 (ahead
     // of its G1 finishes), so its sort passes are not starved by the quotient's NTTs on s0: the
     // witness accumulations start ~5 ms earlier; proof 26.69 -> 26.58 ms (profiles/wplan_r03.txt)
-    for (int k = 0; k < nws_; ++k) {
-      WSet& w = ws_[k];
+    auto build_engines = [&](WSet& w) {
       w.plan = std::make_unique<MsmPlan>(nv, w.pw, s3_);
       for (auto& g : w.g1) g = std::make_unique<MsmEngine>(Curve::G1, w.pw, nv, s2_);
       w.g2 = std::make_unique<MsmEngine>(Curve::G2, w.pw, nv, s1_);
-      wina_ = std::max(wina_, w.g1[0]->window_words());
-      win2_ = std::max(win2_, w.g2->window_words());
-    }
+    };
+    build_engines(ws_[0]);
     plan_h_ = std::make_unique<MsmPlan>(nd, ph, s0_);
     // H scalars are uniform (quotient evaluations): dense plan (one workgroup per sub-bin)
     plan_h_->set_dense(true);
     g1h_ = std::make_unique<MsmEngine>(Curve::G1, ph, nd, s0_);
     winh_ = g1h_->window_words();
+    if (nws_ > 1) {
+      // the second configuration's plan and engines (~6 GB at the Venmo shape) are this pipeline's own:
+      // with many pipelines on one GPU (ZKP_INFLIGHT, a multi-device rehearsal) HBM can run out here,
+      // and the pipeline then keeps the first configuration only (the shared tables stay)
+      try {
+        build_engines(ws_[1]);
+      } catch (const HipError& e) {
+        if (e.code != hipErrorOutOfMemory) throw;
+        (void)hipGetLastError();
+        ws_[1].plan.reset();
+        for (auto& g : ws_[1].g1) g.reset();
+        ws_[1].g2.reset();
+        nws_ = 1;
+      }
+    }
+    for (int k = 0; k < nws_; ++k) {
+      wina_ = std::max(wina_, ws_[k].g1[0]->window_words());
+      win2_ = std::max(win2_, ws_[k].g2->window_words());
+    }
     HIPX(hipMalloc(&dwin_, win_total() * 4));
     HIPX(hipHostMalloc(&hwin_, win_total() * 4, hipHostMallocDefault));
     HIPX(hipStreamSynchronize(s0_));
@@ -521,7 +560,15 @@ class DevicePipeline {
     std::exception_ptr errs[NCOPY];
     std::atomic<uint64_t> sent{0};
     std::atomic<uint32_t> large{0};
-    constexpr int T = NCOPY;
+    // encode threads: every usable host core for a lone upload (the single-proof latency path), the
+    // cores shared out among concurrent uploads (an 8-GPU batch has up to 16 at once: 8 groups of 16
+    // threads encode 705 Venmo witnesses/s on a 16-core quota, of 2 threads 1,096/s;
+    // profiles/host_capacity_r05.json)
+    struct Active {
+      Active() { ++uploads_active_; }
+      ~Active() { --uploads_active_; }
+    } active;
+    const int T = std::max(2, std::min(NCOPY, host_cores() / std::max(1, uploads_active_.load())));
     // chunk c's DMA goes to stream c % NDMA: one copy queue serialises the ~100 chunk copies with
     // ~10 us between them (rocprofv3 --memory-copy-trace: 2.7 ms for 62 MB), parallel queues overlap
     // those gaps and each other's transfers
@@ -919,7 +966,8 @@ class DevicePipeline {
   uint32_t* col_[2] = {nullptr, nullptr};
   uint32_t* val_[2] = {nullptr, nullptr};
   static constexpr int NUP = 2;    // witness upload slots (double buffering)
-  static constexpr int NCOPY = 16;  // host threads per upload (compact encoding into pinned memory, DMA enqueues)
+  static constexpr int NCOPY = 16;  // host threads per upload at most (compact encoding into pinned memory, DMA enqueues)
+  static inline std::atomic<int> uploads_active_{0};  // uploads in progress in this process (all pipelines)
   uint32_t* up_[NUP] = {nullptr, nullptr};      // the witness slots (32 B per signal)
   uint32_t* upstage_[NUP] = {nullptr, nullptr};  // compact chunk regions (HBM)
   uint8_t* uph_[NUP] = {nullptr, nullptr};       // pinned staging of each slot: compact chunk regions
