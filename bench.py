@@ -629,7 +629,9 @@ def main():
     # two pipelines per device sharing the base tables: the batch line keeps two proofs in
     # flight per GPU (+2.4% measured, profiles/inflight_r02.txt); the staged headline runs on
     # each device's first pipeline
-    os.environ.setdefault("ZKP_INFLIGHT", "2")
+    # (a rehearsal maps N logical devices onto one GPU: one pipeline each, or 2N pipelines would share
+    # one GPU's HBM)
+    os.environ.setdefault("ZKP_INFLIGHT", "1" if rehearsal else "2")
     prover = zkp_amd.Prover(zk, devices=devices)
     for d in range(ndev):
         for i, w in enumerate(wit):

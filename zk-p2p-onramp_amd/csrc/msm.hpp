@@ -219,7 +219,8 @@ class MsmEngine {
   // MSM's accumulation while another finishes this one
   void accumulate(const MsmPlan& plan, const MsmBases& bases);
   void finish(const MsmPlan& plan, uint32_t* d_out, hipStream_t st = nullptr);
-  size_t window_words() const { return (size_t)prm_.groups * prm_.K() * 4 * fwords_; }
+  size_t window_words() const { return window_words_for(curve_, prm_); }
+  static size_t window_words_for(Curve c, const MsmParams& p) { return (size_t)p.groups * p.K() * 4 * curve_fwords(c); }
 
   // Kernel instrumentation (HIP events on this engine's stream).  When enabled,
   // every run() brackets the bucket-accumulate kernel with events; collect()

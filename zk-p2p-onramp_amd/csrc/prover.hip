@@ -361,7 +361,7 @@ class DevicePipeline {
       if (share->dev_ != dev_ || share->wlo_ != wlo_ || share->whi_ != whi_ || share->hlo_ != hlo_ ||
           share->hhi_ != hhi_)
         throw ZkpError(ZKP_ERR_INTERNAL, "shared base tables of another device or slice");
-      nws_ = share->nws_;
+      nws_ = share->wset2_tables_ ? 2 : 1;
       for (int k = 0; k < nws_; ++k) {
         const WSet& o = share->ws_[k];
         ws_[k].pw = o.pw, ws_[k].ta = o.ta, ws_[k].tb1 = o.tb1, ws_[k].tc = o.tc, ws_[k].tb2 = o.tb2;
@@ -414,39 +414,47 @@ class DevicePipeline {
     // plans and runs the H MSM.  The witness plan runs on the high-priority finish stream s3 (ahead
     // of its G1 finishes), so its sort passes are not starved by the quotient's NTTs on s0: the
     // witness accumulations start ~5 ms earlier; proof 26.69 -> 26.58 ms (profiles/wplan_r03.txt)
-    auto build_engines = [&](WSet& w) {
-      w.plan = std::make_unique<MsmPlan>(nv, w.pw, s3_);
-      for (auto& g : w.g1) g = std::make_unique<MsmEngine>(Curve::G1, w.pw, nv, s2_);
-      w.g2 = std::make_unique<MsmEngine>(Curve::G2, w.pw, nv, s1_);
-    };
+    nv_ = nv;
     build_engines(ws_[0]);
     plan_h_ = std::make_unique<MsmPlan>(nd, ph, s0_);
     // H scalars are uniform (quotient evaluations): dense plan (one workgroup per sub-bin)
     plan_h_->set_dense(true);
     g1h_ = std::make_unique<MsmEngine>(Curve::G1, ph, nd, s0_);
     winh_ = g1h_->window_words();
-    if (nws_ > 1) {
-      // the second configuration's plan and engines (~6 GB at the Venmo shape) are this pipeline's own:
-      // with many pipelines on one GPU (ZKP_INFLIGHT, a multi-device rehearsal) HBM can run out here,
-      // and the pipeline then keeps the first configuration only (the shared tables stay)
-      try {
-        build_engines(ws_[1]);
-      } catch (const HipError& e) {
-        if (e.code != hipErrorOutOfMemory) throw;
-        (void)hipGetLastError();
-        ws_[1].plan.reset();
-        for (auto& g : ws_[1].g1) g.reset();
-        ws_[1].g2.reset();
-        nws_ = 1;
-      }
-    }
-    for (int k = 0; k < nws_; ++k) {
-      wina_ = std::max(wina_, ws_[k].g1[0]->window_words());
-      win2_ = std::max(win2_, ws_[k].g2->window_words());
+    // the second witness configuration's plan and engines (~6 GB at the Venmo shape) come later
+    // (add_second_wset), after every pipeline of the prover holds its essentials; the group-sum slots
+    // are sized for both
+    wset2_tables_ = nws_ > 1;
+    nws_ = 1;
+    wina_ = ws_[0].g1[0]->window_words();
+    win2_ = ws_[0].g2->window_words();
+    if (wset2_tables_) {
+      const MsmParams& p2 = ws_[1].pw;
+      wina_ = std::max(wina_, MsmEngine::window_words_for(Curve::G1, p2));
+      win2_ = std::max(win2_, MsmEngine::window_words_for(Curve::G2, p2));
     }
     HIPX(hipMalloc(&dwin_, win_total() * 4));
     HIPX(hipHostMalloc(&hwin_, win_total() * 4, hipHostMallocDefault));
     HIPX(hipStreamSynchronize(s0_));
+  }
+
+  // the second witness configuration's plan and engines, this pipeline's own: with many pipelines on
+  // one GPU (ZKP_INFLIGHT, a multi-device rehearsal) HBM can run out here, and the pipeline then keeps
+  // the first configuration only (the shared tables stay).  Called by the Prover once every pipeline
+  // is built.
+  void add_second_wset() {
+    if (!wset2_tables_ || nws_ > 1) return;
+    HIPX(hipSetDevice(dev_));
+    try {
+      build_engines(ws_[1]);
+      nws_ = 2;
+    } catch (const HipError& e) {
+      if (e.code != hipErrorOutOfMemory) throw;
+      (void)hipGetLastError();
+      ws_[1].plan.reset();
+      for (auto& g : ws_[1].g1) g.reset();
+      ws_[1].g2.reset();
+    }
   }
 
   ~DevicePipeline() {
@@ -961,6 +969,13 @@ class DevicePipeline {
   };
   WSet ws_[2];
   int nws_ = 1, wsel_opt_ = 0;
+  bool wset2_tables_ = false;  // this device holds the second configuration's tables (add_second_wset)
+  size_t nv_ = 0;              // witness signals of this pipeline's slice
+  void build_engines(WSet& w) {
+    w.plan = std::make_unique<MsmPlan>(nv_, w.pw, s3_);
+    for (auto& g : w.g1) g = std::make_unique<MsmEngine>(Curve::G1, w.pw, nv_, s2_);
+    w.g2 = std::make_unique<MsmEngine>(Curve::G2, w.pw, nv_, s1_);
+  }
   std::shared_ptr<MsmBases> th_;  // shared by the pipelines of one device
   uint32_t* rowptr_[2] = {nullptr, nullptr};
   uint32_t* col_[2] = {nullptr, nullptr};
@@ -1065,6 +1080,7 @@ Prover::Prover(const uint8_t* zkey, size_t len, const std::vector<int>& devices,
     for (int k = 1; k < inflight_; ++k)
       devs_[(size_t)e * inflight_ + k] = std::make_unique<DevicePipeline>(devs[e], z, part, nparts, first);
   }
+  for (auto& d : devs_) d->add_second_wset();
   // test hooks (never set in production): verify-before-return default, a corrupted H partial
   // (exercises verify-before-return), an injected device failure (exercises the batch re-queue)
   {
