@@ -743,7 +743,7 @@ def main():
         bad2 = [(d, i) for d in range(ndev) for i in range(args.steps) if per_dev[d][i] != refs[i % nw]]
         two = {"proofs_per_s": round(args.steps * ndev / el2, 4), "ms_per_proof": round(el2 / args.steps * 1e3, 3),
                "all_proofs_ok": not bad2, "in_flight_per_device": 2}
-        per_dev[0] = results  # the headline's proofs stay the ones checked below
+        mismatch += [("two in flight", d, i) for d, i in bad2]
     # 1-proof latency, witness in HBM: one staged proof at a time (median of 5)
     lat_st = []
     for i in range(5):
