@@ -714,7 +714,8 @@ class DevicePipeline {
   int witness_sets() const { return nws_; }
   size_t table_bytes() const {
     size_t b = th_->bytes();
-    for (int k = 0; k < nws_; ++k) b += ws_[k].ta->bytes() + ws_[k].tb1->bytes() + ws_[k].tc->bytes() + ws_[k].tb2->bytes();
+    for (int k = 0; k < (wset2_tables_ ? 2 : 1); ++k)  // resident tables, whether or not this pipeline's engines use them
+      b += ws_[k].ta->bytes() + ws_[k].tb1->bytes() + ws_[k].tc->bytes() + ws_[k].tb2->bytes();
     return b;
   }
   // the witness configuration a proof takes: the second (wider windows) when the witness's share of
