@@ -134,6 +134,15 @@ def main(n=300):
         checks.append(("r4lazy_p1tw", lambda z, t=(s02 - s13) * tw: z % R == t * inv_rp_r % R and z < 2 * R))
         checks.append(("r4lazy_p2tw", lambda z, t=(x0 + x2) * tw: z % R == t * inv_rp_r % R and z < 2 * R))
         checks.append(("r4lazy_p3tw", lambda z, t=(x0 - x2) * tw: z % R == t * inv_rp_r % R and z < 2 * R))
+        # the last pair's root w^0 (qreduce only) and the odd-b first radix-2 stage (ntt.hip, round 5)
+        d02, d13 = x0 - x2, (x1 - x3) * wv
+        checks.append(("r4last_d02", lambda z, t=d02: z % R == t % R and z < 6 * R // 5))
+        checks.append(("r4last_p2", lambda z, t=d02 + d13: z % R == t % R and z < 6 * R // 5))
+        checks.append(("r4last_p3", lambda z, t=d02 - d13: z % R == t % R and z < 6 * R // 5))
+        checks.append(("r4last_p2tw", lambda z, t=(d02 + d13) * tw: z % R == t * inv_rp_r % R and z < 2 * R))
+        checks.append(("r4last_p3tw", lambda z, t=(d02 - d13) * tw: z % R == t * inv_rp_r % R and z < 2 * R))
+        checks.append(("r2first_sum", lambda z, t=x0 + x1: z % R == t % R and z < 6 * R // 5))
+        checks.append(("r2first_dif", lambda z, t=(x0 - x1) * wv: z % R == t % R and z < 3 * R))
     # Shoup quotients of the NTT's stage roots (field.hpp shoup_quot) and sub4 against inputs < 4r
     RP_ = 1 << 261
     for wm in [0, 1, R - 1, R - 2] + [rnd.randrange(R) for _ in range(n)]:
@@ -186,6 +195,7 @@ def main(n=300):
     for z in (0, P):
         lines.append("iszq %s" % w8(z)); checks.append(("iszq", lambda v: v == 1))
     out = subprocess.run([BIN], input="\n".join(lines) + "\n", capture_output=True, text=True).stdout.strip().split("\n")
+    assert len(out) == len(checks), (len(out), len(checks))
     bad = {}
     for (name, fn), o in zip(checks, out):
         if name == "iszq":

@@ -52,7 +52,17 @@ int main() {
       prf(mul(add_raw(s02, s13), tw)); printf("\n");              // raw last pair p0 x twiddle (< 2m)
       prf(mul(sub_raw6n(s02, s13), tw)); printf("\n");            // raw p1 x twiddle
       prf(mul(add_raw(x0, x2), tw)); printf("\n");                // raw p2 (d02 + d13, each < 3m)
-      prf(mul(rsub(x0, x2), tw));                                  // raw p3 / odd stage x - y + 4m
+      prf(mul(rsub(x0, x2), tw)); printf("\n");                   // raw p3 / odd stage x - y + 4m
+      // last pair (Hh == 1): d02 = x0 - x2 by the root w^0, only reduced; d13 a Shoup product
+      const Fr d02 = qreduce(rsub(x0, x2)), d13 = mul_shoup(rsub(x1, x3), w, wq);
+      prf(d02); printf("\n");                                       // < 1.2m
+      prf(add(d02, d13)); printf("\n");                             // stored p2
+      prf(sub4(d02, d13)); printf("\n");                            // stored p3 (stage_sub)
+      prf(mul(add_raw(d02, d13), tw)); printf("\n");               // raw p2 x twiddle
+      prf(mul(rsub(d02, d13), tw)); printf("\n");                   // raw p3 x twiddle
+      // odd b's first radix-2 stage (span 2^(b-1)): x0 + x1 and (x0 - x1) w
+      prf(add(x0, x1)); printf("\n");
+      prf(mul_shoup(rsub(x0, x1), w, wq));
     }
     else if (o == "shoupr") {  // a (limbs), w (words, plain), wq (limbs): a w mod r in [0, 3r)
       Fr a = rdl<FrCfg>(), w = rdf<FrCfg>(), wq = rdl<FrCfg>();
