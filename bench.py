@@ -70,10 +70,12 @@ def load_peak():
 
 
 def load_ntt_issue():
-    """Counted NTT issue figures (profiles/ntt_issue_r05.json, the current library: tools/gpu/r5/pmc.sh)."""
+    """Counted NTT issue figures of the current library (profiles/ntt_issue_r05.json, its "current" entry per size:
+    tools/gpu/r5/pmc.sh, ntt_root1.sh)."""
     try:
         with open(os.path.join(ROOT, "profiles", "ntt_issue_r05.json")) as f:
-            return json.load(f)["sizes"]
+            d = json.load(f)
+        return {k: v.get(d.get("current", "cur")) for k, v in d["sizes"].items()}
     except Exception:
         return {}
 
@@ -234,7 +236,7 @@ def ntt_roofline(log_n, ms):
            "frac_vs_issue_ceiling": round(achieved / ISSUE_CEILING_TOPS, 4),
            "hbm_pass_GBps": round(passes * 64 * n / (ms * 1e-3) / 1e9, 1),
            "hbm_frac_of_8TBps": round(passes * 64 * n / (ms * 1e-3) / 8e12, 4)}
-    cnt = load_ntt_issue().get("2^%d" % log_n, {}).get("cur")
+    cnt = load_ntt_issue().get("2^%d" % log_n)
     if cnt:  # counted on the same library (profiles/ntt_issue_r05.json): per-kernel issue at its own clock
         out["valu_lane_instr_per_element_pmc"] = cnt["coset_extension_valu_lane_instr_per_element"]
         out["valu_issue_frac_pmc"] = {k: v["valu_issue_frac"] for k, v in cnt["kernels"].items()}

@@ -42,7 +42,7 @@ def test_ntt_instruction_counts_recompute():
     import pmc_stall
     want = json.load(open(os.path.join(P, "ntt_issue_r05.json")))["sizes"]
     for k in (23, 20):
-        for v in ("base", "cur"):
+        for v in ("base", "cur", "root1"):
             with contextlib.redirect_stdout(io.StringIO()):
                 pmc_stall.ntt(os.path.join(P, "ntt_issue_r05", "ntt%d_%s.csv" % (k, v)), None)
             # recompute per-element counts from the rows directly
@@ -55,6 +55,13 @@ def test_ntt_instruction_counts_recompute():
             assert abs(tot - want["2^%d" % k][v]["coset_extension_valu_lane_instr_per_element"]) < 1.0
     assert want["2^23"]["cur"]["coset_extension_valu_lane_instr_per_element"] < 0.94 * \
         want["2^23"]["base"]["coset_extension_valu_lane_instr_per_element"]
+    # the trivial last-pair root: a quarter product per element per DFT fewer (2^23: six DFTs, 1.5 of 25 products)
+    assert want["2^23"]["root1"]["coset_extension_valu_lane_instr_per_element"] < 0.97 * \
+        want["2^23"]["cur"]["coset_extension_valu_lane_instr_per_element"]
+    import ntt_issue5
+    for k in (23, 20):
+        got = ntt_issue5.entry(os.path.join(P, "ntt_issue_r05", "ntt%d_root1.csv" % k), k)
+        assert got == want["2^%d" % k]["root1"]
 
 
 def test_ubench_peak_is_best_sweep_row():

@@ -124,6 +124,16 @@ __device__ __forceinline__ void root_mul_pair(const Fr& a, uint32_t ja, const Fr
   }
   mul_shoup_pair(a, w, wq, c, v, vq, r, s);
 }
+// a * w_j alone (output < 3m)
+__device__ __forceinline__ Fr root_mul(const Fr& a, uint32_t j, const uint32_t* __restrict__ ltw) {
+  Fr w, wq;
+#pragma unroll
+  for (int l = 0; l < NL; ++l) {
+    w.v[l] = ltw[l * MAX_TW + j];
+    wq.v[l] = ltw[(NL + l) * MAX_TW + j];
+  }
+  return mul_shoup(a, w, wq);
+}
 
 // one radix-4 unit (thread work item q) of round t: rows r0 + {0, H/2, H, 3H/2} of stage t
 // (span H) and t+1 (span H/2), r0 = grp 2H + i.
@@ -153,10 +163,18 @@ __device__ __forceinline__ void r4_unit(uint32_t* __restrict__ lds, const uint32
   // stage t: (x0, x2) with w_(2H)^i, (x1, x3) with w_(2H)^(i + H/2); stage t+1: (s02, s13)
   // and (d02, d13), both with w_H^i.  Roots as exponents of w_(2^b) (stage t: i << t).
   // the unit's independent root products in lockstep pairs (d02 / d13, then y1 / y3 by the same
-  // root); every lane multiplies (w^0 = 1 for i = 0: no divergent j == 0 path)
+  // root); inside a round every lane multiplies (w^0 = 1 for i = 0: no divergent j == 0 path).  The
+  // last pair of a DFT (Hh == 1, a round-uniform branch; odd b too, dft_stages) has i = 0 for every lane: stage t's
+  // first difference takes w^0 = 1 and is only reduced (qreduce: < 1.2m, ~43 instructions instead of
+  // half a lockstep Shoup pair)
   const uint32_t j = i << (t + 1);
   Fr d02, d13;
-  root_mul_pair(rsub(x0, x2), i << t, rsub(x1, x3), (i + Hh) << t, ltw, d02, d13);
+  if (Hh > 1) {
+    root_mul_pair(rsub(x0, x2), i << t, rsub(x1, x3), (i + Hh) << t, ltw, d02, d13);
+  } else {
+    d02 = qreduce(rsub(x0, x2));
+    d13 = root_mul(rsub(x1, x3), 1u << t, ltw);
+  }
   const Fr s02 = add_raw(x0, x2), s13 = add_raw(x1, x3);  // < 6m, limbs < 2^30
   if (Hh > 1) {
     lds_put<LE>(lds, E, p0, add_raw_reduce(s02, s13));
@@ -179,19 +197,54 @@ __device__ __forceinline__ void r4_unit(uint32_t* __restrict__ lds, const uint32
 }
 
 // b radix-2 DIF stages on the LDS tile (rows natural in, bit-reversed out), done two at a
-// time as radix-4 groups in registers (half the LDS traffic and barriers of radix-2).  raw: the
-// outputs feed a Montgomery product only (r4_unit)
+// time as radix-4 groups in registers (half the LDS traffic and barriers of radix-2), an odd b's
+// extra stage first.  raw: the outputs feed a Montgomery product only (r4_unit).  Every access
+// phase stays bank-conflict-free under swz (simulated for the 2^12..2^23 geometries, both orders)
 template <int LE>
 __device__ __forceinline__ void dft_stages(uint32_t* __restrict__ lds, const uint32_t* __restrict__ ltw, int E_rt,
                                            int b, int lc, bool raw) {
   const int E = LE ? (1 << LE) : E_rt;
   const uint32_t C = 1u << lc;
   int t = 0;
+  if ((b & 1) && b > 1) {
+    // odd b: the lone radix-2 stage goes FIRST (span 2^(b-1), roots w_(2^b)^r), so that the radix-4
+    // rounds end on a span-2/span-1 pair whose stage-t root is w^0 (r4_unit, Hh == 1): 0.25 products
+    // per element fewer than a radix-4 run ending on the root-free span-1 stage.  Two pairs per
+    // thread in lockstep; outputs < 1.2m (qreduce) and < 3m (Shoup), normalised
+    const uint32_t half = 1u << (b - 1);
+    const int stp = swz((int)(half << lc));
+    auto pos = [&](int q, uint32_t& r) {
+      const uint32_t col = (uint32_t)q & (C - 1);
+      r = ((uint32_t)q >> lc) & (half - 1);
+      const uint32_t bl = (uint32_t)q >> (lc + b - 1);
+      return swz((int)(bl << (b + lc)) + (int)(r << lc) + (int)col);
+    };
+    for (int q = threadIdx.x; q < (E >> 1); q += 2 * NTT_TPB) {
+      uint32_t ra, rc;
+      const int a0 = pos(q, ra), a1 = a0 ^ stp;
+      const Fr x0 = lds_get<LE>(lds, E, a0), x1 = lds_get<LE>(lds, E, a1);
+      if (q + NTT_TPB < (E >> 1)) {
+        const int c0 = pos(q + NTT_TPB, rc), c1 = c0 ^ stp;
+        const Fr y0 = lds_get<LE>(lds, E, c0), y1 = lds_get<LE>(lds, E, c1);
+        Fr u, v;
+        root_mul_pair(rsub(x0, x1), ra, rsub(y0, y1), rc, ltw, u, v);
+        lds_put<LE>(lds, E, a0, add(x0, x1));
+        lds_put<LE>(lds, E, a1, u);
+        lds_put<LE>(lds, E, c0, add(y0, y1));
+        lds_put<LE>(lds, E, c1, v);
+      } else {
+        lds_put<LE>(lds, E, a1, root_mul(rsub(x0, x1), ra, ltw));
+        lds_put<LE>(lds, E, a0, add(x0, x1));
+      }
+    }
+    __syncthreads();
+    t = 1;
+  }
   for (; t + 1 < b; t += 2) {
     for (int q = threadIdx.x; q < (E >> 2); q += NTT_TPB) r4_unit<LE>(lds, ltw, E, b, lc, t, q, raw);
     __syncthreads();
   }
-  if (t < b) {  // odd b: the last radix-2 stage (span 1)
+  if (t < b) {  // b == 1: the one radix-2 stage (span 1)
     for (int q = threadIdx.x; q < (E >> 1); q += NTT_TPB) {
       const uint32_t col = (uint32_t)q & (C - 1), bq = ((uint32_t)q >> lc) & ((1u << (b - 1)) - 1);
       const uint32_t bl = (uint32_t)q >> (lc + b - 1);
