@@ -376,10 +376,15 @@ def batch_pcie_inclusive(args, circ, prover, wit, refs, rank, world, ndev, dist,
     if dist:
         dist.barrier()
     sync()
+    rx = roctx()  # a "batch timed" range for a profiler (tools/prof/batch_gaps.py)
+    if rx:
+        rx.roctxRangePushA(b"batch timed")
     t0 = time.perf_counter()
     res = prover.prove_batch_raw([host[i] for i in order], [r_fix] * len(order), [s_fix] * len(order))
     sync()
     el = time.perf_counter() - t0
+    if rx:
+        rx.roctxRangePop()
     if dist:
         import torch
         t = torch.tensor([el], dtype=torch.float64)

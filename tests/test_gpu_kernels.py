@@ -174,6 +174,20 @@ def test_ntt_golden(golden_dir, k):
     assert zkp_amd.ntt_fr(a, 2) == [int(x) for x in d["coset"]]
 
 
+@pytest.mark.parametrize("k", [2, 3, 5, 6, 7, 8, 9, 11, 13, 15])
+def test_ntt_every_pass_geometry(k):
+    """Forward, inverse and coset extension against the oracle's radix-2 NTT for pass splits with odd
+    and even pass widths (3: b = 3; 5, 7: one odd pass; 9 = 5 + 4; 11 = 6 + 5; 13 = 7 + 6; 15 = 8 + 7) and
+    tiles smaller than 1024 elements: the odd pass's radix-2 stage runs first and every DFT's last
+    radix-4 pair skips its w^0 product (ntt.hip, round 5)"""
+    rng = circuit.SplitMix64(100 + k, 3)
+    a = [rng.fr() for _ in range(1 << k)]
+    assert zkp_amd.ntt_fr(a, 0) == ntt.fft(a)
+    inv_a = ntt.ifft(a)
+    assert zkp_amd.ntt_fr(a, 1) == inv_a
+    assert zkp_amd.ntt_fr(a, 2) == ntt.fft(ntt.batch_apply_key(inv_a, 1, ntt.coset_gen(1 << k)))
+
+
 @pytest.mark.parametrize("k", [14, 17, 20])
 def test_ntt_roundtrip_large(k):
     rng = circuit.SplitMix64(k, 2)
