@@ -27,6 +27,7 @@ events), and the C++ CPU restatement (oracle/cpu) timed on this host as cpu_base
 """
 import argparse
 import ctypes
+import gc
 import json
 import os
 import sys
@@ -376,6 +377,7 @@ def batch_pcie_inclusive(args, circ, prover, wit, refs, rank, world, ndev, dist,
     if dist:
         dist.barrier()
     sync()
+    quiesce_gc()
     rx = roctx()  # a "batch timed" range for a profiler (tools/prof/batch_gaps.py)
     if rx:
         rx.roctxRangePushA(b"batch timed")
@@ -403,6 +405,17 @@ def batch_pcie_inclusive(args, circ, prover, wit, refs, rank, world, ndev, dist,
             "note": "zkp_prove_batch from pageable host memory over %d device(s): the compact transfer of "
                     "witness i+1 (16 encode threads, pinned staging, 4 copy queues) runs while proof i computes"
                     % ndev}
+
+
+def quiesce_gc():
+    """Collect, then move every live Python object to the permanent generation (gc.freeze) before a
+    timed region.  The harness holds millions of long-lived objects (synthetic circuit, witnesses,
+    reference proofs); a full collection triggered by the batch binding's few hundred result objects
+    walks all of them and stalled a 256-proof batch for 215-260 ms before its first or after its last
+    kernel (profiles/batch_gc_r05.txt) -- a harness artefact, not the prover's (the C ABI allocates no
+    Python objects)."""
+    gc.collect()
+    gc.freeze()
 
 
 def roctx():
@@ -712,6 +725,7 @@ def main():
             if errs:
                 raise errs[0]
         per_dev[d] = out
+    quiesce_gc()
     rx = roctx()  # a "bench timed" range in a rocprofv3 --marker-trace (tools/prof/launch_split.py)
     if rx:
         rx.roctxRangePushA(b"bench timed")

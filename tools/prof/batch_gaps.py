@@ -59,13 +59,23 @@ def summarize(rows, t0, t1):
         if k:
             dur[k].append((e - s) / 1e6)
     acc = {k: v for k, v in dur.items() if k.startswith("k_accumulate (grid")}
+    # drift over the range: per tenth of the span, the proofs started and the median H-launch time
+    # (the accumulate grid with the longest launches), to separate a steady cost from a slow clock-down
+    hk = max(acc, key=lambda k: statistics.median(acc[k])) if acc else None
+    deciles = []
+    for q in range(10):
+        a, b = t0 + span * q // 10, t0 + span * (q + 1) // 10
+        hs = [(e - s) / 1e6 for s, e, n, g, w in ks if a <= s < b and kind(n, g, w) == hk]
+        deciles.append({"proofs_started": sum(1 for s, _, n, _, _ in ks if a <= s < b and "k_build_abc" in n),
+                        "h_launch_median_ms": round(statistics.median(hs), 3) if hs else None})
     # the H launch: the accumulate grid with the most additions ~ the largest median duration
     return {"span_ms": round(span / 1e6, 2), "proofs": proofs,
             "ms_per_proof": round(span / 1e6 / proofs, 3) if proofs else None,
             "gpu_busy_frac": round(busy / span, 4), "idle_ms_per_proof": round((span - busy) / 1e6 / max(proofs, 1), 3),
             "idle_in_gaps_over_0.1ms_per_proof": round(sum(g for g in gaps if g > 100000) / 1e6 / max(proofs, 1), 3),
             "kernel_median_ms": {k: round(statistics.median(v), 4) for k, v in sorted(dur.items()) if len(v) >= 3},
-            "accumulate_grids": sorted(acc, key=lambda k: -statistics.median(acc[k]))}
+            "accumulate_grids": sorted(acc, key=lambda k: -statistics.median(acc[k])),
+            "by_tenth_of_span": deciles}
 
 
 def main(trace_csv, marker_csv, out=None):
