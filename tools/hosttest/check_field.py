@@ -143,6 +143,10 @@ def main(n=300):
         checks.append(("r4last_p3tw", lambda z, t=(d02 - d13) * tw: z % R == t * inv_rp_r % R and z < 2 * R))
         checks.append(("r2first_sum", lambda z, t=x0 + x1: z % R == t % R and z < 6 * R // 5))
         checks.append(("r2first_dif", lambda z, t=(x0 - x1) * wv: z % R == t % R and z < 3 * R))
+        checks.append(("shouptw_p0", lambda z, t=(s02 + s13) * wv: z % R == t % R and z < 3 * R))
+        checks.append(("shouptw_p2", lambda z, t=(x0 + x2) * wv: z % R == t % R and z < 3 * R))
+        checks.append(("shouptw_last_p2", lambda z, t=(d02 + d13) * wv: z % R == t % R and z < 3 * R))
+        checks.append(("shouptw_last_p3", lambda z, t=(d02 - d13) * wv: z % R == t % R and z < 3 * R))
     # Shoup quotients of the NTT's stage roots (field.hpp shoup_quot) and sub4 against inputs < 4r
     RP_ = 1 << 261
     for wm in [0, 1, R - 1, R - 2] + [rnd.randrange(R) for _ in range(n)]:

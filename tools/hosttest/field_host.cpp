@@ -62,7 +62,12 @@ int main() {
       prf(mul(rsub(d02, d13), tw)); printf("\n");                   // raw p3 x twiddle
       // odd b's first radix-2 stage (span 2^(b-1)): x0 + x1 and (x0 - x1) w
       prf(add(x0, x1)); printf("\n");
-      prf(mul_shoup(rsub(x0, x1), w, wq));
+      prf(mul_shoup(rsub(x0, x1), w, wq)); printf("\n");
+      // raw last-round outputs into the Shoup twiddle / coset-key products (round 5 tables)
+      prf(mul_shoup(add_raw(s02, s13), w, wq)); printf("\n");
+      prf(mul_shoup(add_raw(x0, x2), w, wq)); printf("\n");
+      prf(mul_shoup(add_raw(d02, d13), w, wq)); printf("\n");
+      prf(mul_shoup(rsub(d02, d13), w, wq));
     }
     else if (o == "shoupr") {  // a (limbs), w (words, plain), wq (limbs): a w mod r in [0, 3r)
       Fr a = rdl<FrCfg>(), w = rdf<FrCfg>(), wq = rdl<FrCfg>();
