@@ -12,7 +12,7 @@ import pathlib
 import pytest
 
 PROFILES = pathlib.Path(__file__).resolve().parent.parent / "profiles"
-LINES = ["bench_r01.json", "bench_r01_recheck.json"]
+LINES = ["bench_r01.json", "bench_r01_recheck.json", "bench_r05_final.json"]
 REQUIRED = ["metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
             "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"]
 
@@ -73,3 +73,23 @@ def test_gpus_more_than_visible_fails_loudly():
     assert p.returncode == 2, (p.returncode, p.stderr[-2000:])
     assert "--gpus 64 requested" in p.stderr and "--rehearsal" in p.stderr
     assert p.stdout.strip() == ""
+
+
+def test_round5_line_fields():
+    """The round-5 default bench line (profiles/bench_r05_final.json) carries what VERDICT r4 asked for:
+    verified batch proofs, the counted VALU issue and clock beside the H roofline, the issue-ceiling
+    fraction consistent with `achieved`, the fixed-base label of the MSM kernel line with its table
+    build time, and the NTT's counted instructions per element."""
+    d = _load("bench_r05_final.json")
+    b = d["batch_pcie_inclusive"]
+    assert b["verified"] == "%d/%d" % (b["proofs_per_rank"], b["proofs_per_rank"]) and b["all_proofs_ok"]
+    assert b["verify_before_return_mode"] == 2 and b["vs_staged_headline"] > 0.95
+    r = d["roofline"]
+    assert 0.9 < r["valu_issue_frac_pmc"] < 1.0 and 1.5 < r["clock_GHz_pmc"] < 2.5
+    assert r["frac_vs_issue_ceiling"] == pytest.approx(r["achieved"] / r["issue_ceiling"], rel=1e-3)
+    assert r["issue_ceiling"] == pytest.approx(256 * 64 * 2.4e9 / 1e12, rel=1e-4)
+    k = d["kernels_config1"]
+    assert k["msm_kind"].startswith("fixed-base") and k["msm_g1_2^20_table_build_ms"] > 0
+    ntt = k["ntt_roofline"]["2^23 (Venmo domain)"]
+    assert ntt["valu_lane_instr_per_element_pmc"] < 6000
+    assert d["all_proofs_ok"] and d["cpu_baseline"]["bit_exact_vs_gpu"]
