@@ -131,7 +131,7 @@ static int env_int(const char* name, int dflt) {
 //   w=<bits>  h=<bits>    window bits of the witness plan / the H plan (8..24)
 //   depth=<rows>          base-table rows T per point (1..W; default W, or the largest depth whose
 //                         tables fit half of the free HBM)
-//   task_w=<n> task_h=<n> entries per bucket-accumulation task of either plan (default 32)
+//   task_w=<n> task_h=<n> entries per bucket-accumulation task of either plan (default 32 / 48)
 //   seg=<n>               buckets per bucket-reduction segment (a power of two; default 4)
 //   plan=dense|compact    the plan variant of the kernel-level MSMs (zkp_msm_*; default dense)
 // A malformed value or an unknown key is a ZKP_ERR_INVALID_ARG: a typo never silently tunes nothing.
@@ -217,6 +217,11 @@ static void choose_msm_params(size_t n_w, size_t n_h, const MsmOptions& o, MsmPa
   };
   pw = make_params(n_w, cw, o.depth);
   ph = make_params(n_h, ch, o.depth);
+  // H-plan tasks of <= 48 entries (the uniform quotient scalars fill every bucket evenly, ~208 entries at
+  // the Venmo shape: 5 task partials per bucket instead of 7, so the latency-bound merge_final at the end
+  // of the proof folds fewer): +0.7 % and +0.9 % proofs/s over 32, 7 of 7 alternated rounds on two boxes
+  // (profiles/task_size_ab_r05.txt); the witness plan keeps 32 (its 0/1-heavy buckets: 64 measured -0.5 %)
+  ph.S = 48;
   tune();
   if (o.depth > 0) return;
   size_t free_b = 0, total_b = 0;
