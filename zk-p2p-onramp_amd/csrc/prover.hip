@@ -209,19 +209,18 @@ static void choose_msm_params(size_t n_w, size_t n_h, const MsmOptions& o, MsmPa
   auto clampc = [](int c) { return c < 8 ? 8 : (c > 20 ? 20 : c); };
   const int cw = o.w ? o.w : clampc(lg(n_w) - 5);
   const int ch = o.h ? o.h : dense_window_bits(clampc(lg(n_h) - 3), n_h);
+  // H-plan tasks of <= 48 entries (the uniform quotient scalars fill every bucket evenly, ~208 entries at
+  // the Venmo shape: 5 task partials per bucket instead of 7, so the latency-bound merge_final at the end
+  // of the proof folds fewer): +0.7 % and +0.9 % proofs/s over 32, 7 of 7 alternated rounds on two boxes
+  // (profiles/task_size_ab_r05.txt); the witness plan keeps 32 (its 0/1-heavy buckets: 24-64 within noise)
   auto tune = [&] {
     if (o.task_w > 0) pw.S = o.task_w;
-    if (o.task_h > 0) ph.S = o.task_h;
+    ph.S = o.task_h > 0 ? o.task_h : 48;
     for (MsmParams* q : {&pw, &ph})
       if (o.seg > 0 && o.seg <= (1 << (q->c - 1))) q->M = o.seg;
   };
   pw = make_params(n_w, cw, o.depth);
   ph = make_params(n_h, ch, o.depth);
-  // H-plan tasks of <= 48 entries (the uniform quotient scalars fill every bucket evenly, ~208 entries at
-  // the Venmo shape: 5 task partials per bucket instead of 7, so the latency-bound merge_final at the end
-  // of the proof folds fewer): +0.7 % and +0.9 % proofs/s over 32, 7 of 7 alternated rounds on two boxes
-  // (profiles/task_size_ab_r05.txt); the witness plan keeps 32 (its 0/1-heavy buckets: 64 measured -0.5 %)
-  ph.S = 48;
   tune();
   if (o.depth > 0) return;
   size_t free_b = 0, total_b = 0;
