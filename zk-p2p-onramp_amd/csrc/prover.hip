@@ -1588,6 +1588,7 @@ struct MsmRig {
       const MsmOptions opt = msm_options();
       const int c_auto = dense_window_bits(std::min(20, std::max(8, lg - 3)), n);
       prm = make_params(std::max<size_t>(n, 1), c ? c : c_auto, depth);
+      prm.S = opt.task_h > 0 ? opt.task_h : 48;  // the H plan's task size too (choose_msm_params)
       bases = std::make_unique<MsmBases>(curve, n, prm.c, prm.depth);
       hipEvent_t t0, t1;
       HIPX(hipEventCreate(&t0));
