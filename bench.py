@@ -559,6 +559,100 @@ def cpu_baseline(args, zk, wit0, gpu_proof, r_fix, s_fix, msm_case):
         return {"value": None, "error": str(e), "host": info, "published": PUBLISHED_CPU}
 
 
+def sustained_line(args, prover, ndev, nw, refs, dist, sync, on_devices, r_fix, s_fix):
+    """The staged headline loop run for >= args.sustain_s seconds: one proof at a time
+    per device, every proof compared with the reference proof of its witness.  The 20-step headline is a
+    ~0.5-s window on a chip that runs power-limited (1.8-2.3 GHz under these kernels); this
+    is the node-throughput figure over ~1,250 proofs."""
+    counts = [0] * ndev
+    bad = []
+    stop = [False]
+
+    def loop(d):
+        i = 0
+        while not stop[0]:
+            pr = prover.prove_staged_raw(i % nw, r_fix, s_fix, dev_index=d)
+            if pr != refs[i % nw]:
+                bad.append((d, i))
+            i += 1
+        counts[d] = i
+    if dist:
+        dist.barrier()
+    sync()
+    quiesce_gc()
+    timer = threading.Timer(args.sustain_s, lambda: stop.__setitem__(0, True))
+    t0 = time.perf_counter()
+    timer.start()
+    on_devices(loop)
+    sync()
+    el = time.perf_counter() - t0
+    timer.cancel()
+    n = sum(counts)
+    if dist:
+        import torch
+        t = torch.tensor([el], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+        t = torch.tensor([float(n)], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        n = int(t.item())
+    return {"proofs_per_s": round(n / el, 3), "proofs": n, "seconds": round(el, 2),
+            "ms_per_proof": round(el / max(1, n) * 1e3 * ndev, 3), "all_proofs_ok": not bad,
+            "mismatched_proofs": bad[:8],
+            "note": "staged loop, one proof at a time per device, for >= %.0f s; every proof checked" % args.sustain_s}
+
+
+def compact_line(out):
+    """The contract line the driver keeps (its record holds the last 8 KB of stdout):
+    the metric's two halves (proofs/s and 1-proof latency), the sustained and batch rates, the headline
+    roofline and cpu_baseline, and the configs[1] kernel numbers.  Everything else is in the
+    {"bench_detail": ...} line printed just before it."""
+    keep = ["metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "latency_ms", "latency_ms_staged",
+            "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "value_note", "all_proofs_ok",
+            "rehearsal"]
+    c = {k: out[k] for k in keep if k in out}
+    cfg = out.get("config", {})
+    c["config"] = {k: cfg[k] for k in ("workload", "n_vars", "n_constraints", "n_public", "domain",
+                                      "witness_bool_pct", "parallelism") if k in cfg}
+    su = out.get("sustained")
+    if su:
+        c["sustained"] = {k: su.get(k) for k in ("proofs_per_s", "proofs", "seconds", "vs_value", "all_proofs_ok")}
+    b = out.get("batch_pcie_inclusive")
+    if b:
+        c["batch_pcie_inclusive"] = {k: b.get(k) for k in ("proofs_per_s", "proofs_per_rank", "verified",
+                                                          "vs_staged_headline", "all_proofs_ok")}
+    two = out.get("staged_two_in_flight")
+    if two:
+        c["staged_two_in_flight_proofs_per_s"] = two.get("proofs_per_s")
+    r = out.get("roofline") or {}
+    c["roofline"] = {k: r[k] for k in ("kernel", "bound", "achieved", "peak", "unit", "frac", "traffic",
+                                      "algorithmic_work_per_launch", "avg_launch_ms", "launches_timed",
+                                      "valu_issue_frac_pmc", "valu_busy_weighted_pmc", "clock_GHz_pmc",
+                                      "frac_vs_issue_ceiling", "issue_ceiling", "hbm_GBps", "peak_source")
+                     if k in r}
+    g2 = (out.get("roofline_launches") or {}).get("roofline_g2")
+    if g2:
+        c["roofline_g2_frac"] = g2.get("frac")
+    cb = out.get("cpu_baseline")
+    if cb:
+        c["cpu_baseline"] = {k: cb.get(k) for k in ("value", "unit", "cores", "kind", "label", "sample",
+                                                   "bit_exact_vs_gpu", "error") if k in cb}
+    au = out.get("all_uniform_witness")
+    if au:
+        c["all_uniform_witness"] = {k: au.get(k) for k in ("proofs_per_s", "ms_per_proof", "all_proofs_ok")}
+    kb = out.get("kernels_config1")
+    if kb:
+        nr = kb.get("ntt_roofline", {})
+        c["kernels_config1"] = {
+            "msm_g1_2^20_Mpts_per_s": kb.get("msm_g1_2^20_Mpts_per_s"), "msm_g1_2^20_ms": kb.get("msm_g1_2^20_ms"),
+            "msm_kind": "fixed-base (table build %s ms, outside)" % kb.get("msm_g1_2^20_table_build_ms"),
+            "ntt_2^20_ms": (nr.get("2^20") or {}).get("ms"), "ntt_2^20_frac": (nr.get("2^20") or {}).get("frac"),
+            "ntt_2^23_ms": (nr.get("2^23 (Venmo domain)") or {}).get("ms"),
+            "ntt_2^23_frac": (nr.get("2^23 (Venmo domain)") or {}).get("frac")}
+    c["detail"] = "the {\"bench_detail\": ...} stdout line before this one (per-launch rooflines, stage ms, PMC)"
+    return c
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -587,6 +681,11 @@ def main():
                     help="staged proofs in flight per device in the timed loop (host threads per device, up to "
                          "ZKP_INFLIGHT pipelines).  1 (default) keeps every accumulate launch's time its own (the "
                          "per-launch rooflines); the line also reports 2 in flight as staged_two_in_flight")
+    ap.add_argument("--sustain-s", type=float, default=30.0,
+                    help="seconds of the sustained staged loop reported beside the 20-step headline (0 = skip)")
+    ap.add_argument("--detail-out", default="",
+                    help="also write the detailed JSON object to this file (it is always printed as an earlier "
+                         "stdout line {\"bench_detail\": ...}; the last line is the compact contract line)")
     ap.add_argument("--rehearsal", action="store_true",
                     help="--gpus N without torchrun on fewer GPUs: N logical devices on one GPU (code-path check; "
                          "the line says \"rehearsal\": true and is not a scaling number)")
@@ -792,6 +891,10 @@ def main():
     if args.batch > 0:
         batch = batch_pcie_inclusive(args, circ, prover, wit, refs, rank, world, ndev, dist, sync, R_FIX, S_FIX)
 
+    sustained = None
+    if args.sustain_s > 0:
+        sustained = sustained_line(args, prover, ndev, nw, refs, dist, sync, on_devices, R_FIX, S_FIX)
+
     if rank != 0:
         return
 
@@ -844,6 +947,7 @@ def main():
         "proof_check": "every timed proof == the reference proof of the same staged witness (device 0, same r, s)",
         "stage_ms_last_proof": {k: round(v, 3) for k, v in stage_ms.items()},
         "batch_pcie_inclusive": batch,
+        "sustained": sustained,
         "roofline": roofline,
         "roofline_launches": acc_lines,
     }
@@ -872,7 +976,18 @@ def main():
 
     if args.cpu_baseline == "full":
         out["cpu_baseline"] = cpu_baseline(args, zk, wit[0], results[0][0], R_FIX, S_FIX, msm_case)
-    print(json.dumps(out), flush=True)
+    if sustained:
+        sustained["vs_value"] = round(sustained["proofs_per_s"] / value, 4)
+        if sustained["vs_value"] < 0.98:
+            out["value_note"] = ("the %.0f-s sustained staged loop ran at %.4f of `value` (%.2f proofs/s): the chip "
+                                 "runs power-limited under these kernels; node throughput over minutes is the "
+                                 "sustained figure" % (sustained["seconds"], sustained["vs_value"],
+                                                       sustained["proofs_per_s"]))
+    print(json.dumps({"bench_detail": out}), flush=True)
+    if args.detail_out:
+        with open(args.detail_out, "w") as f:
+            json.dump(out, f)
+    print(json.dumps(compact_line(out)), flush=True)
 
 
 if __name__ == "__main__":

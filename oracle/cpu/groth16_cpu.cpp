@@ -413,6 +413,50 @@ int g16cpu_msm_g2(const uint8_t* pts, const uint8_t* sc, size_t n, int threads, 
   return 0;
 }
 
+// Standalone Fr NTT of n = 2^k standard-form LE values (< r), natural order in and out, the
+// transforms of snarkjs groth16_prove (the loop in g16cpu_prove below):
+// mode 0 Fr.fft (w = Fr.w[k]), 1 Fr.ifft (w^-1, times 1/n), 2 the coset extension
+// ifft -> batchApplyKey(1, Fr.w[k+1]) -> fft.  in and out may alias.
+int g16cpu_ntt(const uint8_t* in, size_t n, int mode, int threads, uint8_t* out) {
+  if (n == 0 || (n & (n - 1)) || n > (size_t(1) << 27) || mode < 0 || mode > 2) return 1;
+  int lg = 0;
+  while ((size_t(1) << lg) < n) ++lg;
+  std::vector<Fr> a(n);
+  par(threads, n, [&](size_t lo, size_t hi, int) {
+    for (size_t i = lo; i < hi; ++i) a[i] = Fr::from_std(Fr::from_raw(in + 32 * i));
+  });
+  const Fr wr = root(lg), winv = wr.inv(), ninv = fr_u64(n).inv();
+  if (mode == 0) {
+    ntt(a, wr, threads);
+  } else {
+    ntt(a, winv, threads);
+    if (mode == 1) {
+      par(threads, n, [&](size_t lo, size_t hi, int) {
+        for (size_t i = lo; i < hi; ++i) a[i] = a[i] * ninv;
+      });
+    } else {
+      // key ninv * g^i, g = Fr.w[k+1]: each thread starts its run at g^lo
+      const Fr g = root(lg + 1);
+      par(threads, n, [&](size_t lo, size_t hi, int) {
+        u64 e[4] = {lo, 0, 0, 0};
+        Fr cur = g.pow(e) * ninv;
+        for (size_t i = lo; i < hi; ++i) {
+          a[i] = a[i] * cur;
+          cur = cur * g;
+        }
+      });
+      ntt(a, wr, threads);
+    }
+  }
+  par(threads, n, [&](size_t lo, size_t hi, int) {
+    for (size_t i = lo; i < hi; ++i) {
+      Fr v = a[i].to_std();
+      std::memcpy(out + 32 * i, v.v, 32);
+    }
+  });
+  return 0;
+}
+
 // Full Groth16 proof.  out: A (64) | B (128) | C (64) standard-form LE.  ms[0..4]:
 // buildABC, NTT+join, MSM G1, MSM G2, total.
 int g16cpu_prove(const uint8_t* zk, size_t zlen, const uint8_t* wt, size_t wlen, const uint8_t* r32,

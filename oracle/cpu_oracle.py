@@ -21,6 +21,7 @@ def lib():
                                    ctypes.c_void_p, ctypes.POINTER(ctypes.c_double)]
         L.g16cpu_msm_g1.argtypes = [u8p, u8p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]
         L.g16cpu_msm_g2.argtypes = [u8p, u8p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]
+        L.g16cpu_ntt.argtypes = [u8p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
         _lib = L
     return _lib
 
@@ -55,3 +56,14 @@ def msm_g2(points: bytes, scalars: bytes, threads: int = 8):
     lib().g16cpu_msm_g2(points, scalars, len(scalars) // 32, threads, out)
     v = _ints(out.raw, 4)
     return None if v == [0, 0, 0, 0] else ((v[0], v[1]), (v[2], v[3]))
+
+
+def ntt(values: bytes, mode: int, threads: int = 8) -> bytes:
+    """Fr NTT of len(values) // 32 standard-form LE values (a power of two): mode 0 Fr.fft, 1 Fr.ifft,
+    2 the coset extension ifft -> batchApplyKey(1, Fr.w[k+1]) -> fft (groth16_cpu.cpp g16cpu_ntt).
+    Returns the outputs in the same layout."""
+    n = len(values) // 32
+    out = ctypes.create_string_buffer(len(values))
+    if lib().g16cpu_ntt(values, n, mode, threads, out) != 0:
+        raise ValueError("g16cpu_ntt: n must be a power of two <= 2^27 and mode 0..2")
+    return out.raw

@@ -42,3 +42,23 @@ def test_cpu_port_msm_g2(co):
     e = blob[n * 160:]
     v = [bn254.le_to_int(e[32 * i:32 * i + 32]) for i in range(4)]
     assert co.msm_g2(blob[:n * 128], blob[n * 128:n * 160], threads=4) == ((v[0], v[1]), (v[2], v[3]))
+
+
+@pytest.mark.parametrize("k", [1, 4, 10, 12])
+def test_cpu_port_ntt_golden(co, k):
+    """The standalone NTT export (g16cpu_ntt, the checker of the 2^20 / 2^23 GPU NTT tests) against the
+    golden vectors: forward, inverse and coset extension."""
+    d = json.load(open(os.path.join(GOLD, "ntt_%d.json" % k)))
+    raw = b"".join(int(x).to_bytes(32, "little") for x in d["input"])
+
+    def dec(b):
+        return [bn254.le_to_int(b[32 * i:32 * i + 32]) for i in range(len(b) // 32)]
+    for mode, key in ((0, "forward"), (1, "inverse"), (2, "coset")):
+        assert dec(co.ntt(raw, mode, threads=4)) == [int(x) for x in d[key]], key
+
+
+def test_cpu_port_ntt_rejects_bad_sizes(co):
+    with pytest.raises(ValueError):
+        co.ntt(b"\0" * 96, 0)
+    with pytest.raises(ValueError):
+        co.ntt(b"\0" * 64, 3)

@@ -748,6 +748,15 @@ def ntt_fr(values, mode: int, device: int = 0):
     return [_le(out[32 * i:32 * i + 32]) for i in range(len(values))]
 
 
+def ntt_fr_bytes(raw, mode: int, device: int = 0) -> bytes:
+    """As ntt_fr on len(raw) // 32 standard-form LE values (< r) given as bytes; returns bytes of the same
+    layout (no per-element Python integers: the 2^20 / 2^23 parity tests)."""
+    lib = load_library()
+    arr = (ctypes.c_uint8 * len(raw)).from_buffer_copy(raw)
+    _check(lib.zkp_ntt_fr(device, ctypes.cast(arr, ctypes.POINTER(ctypes.c_uint8)), len(raw) // 32, mode))
+    return bytes(arr)
+
+
 def bench_msm(points_lem: bytes, scalars_le: bytes, g2: bool = False, warmup: int = 2, iters: int = 10,
               device: int = 0):
     """Device-resident MSM timing (HIP events on the engine stream).  Returns (stats dict, result)."""
