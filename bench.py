@@ -54,7 +54,10 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-ISSUE_CEILING_TOPS = 256 * 64 * 2.4e9 / 1e12  # one wave64 VALU instruction per SIMD per 4 clocks at 2.4 GHz
+# one wave64 v_mad_u64_u32 per SIMD per quad-cycle (4 clocks) at 2.4 GHz: the 4-clock class, which is every
+# instruction of the field products; the 2-clock class (v_and/add/sub/mov/lshrrev_b32 e32) shares a quad-cycle
+# only with another wave's 2-clock instruction (profiles/valu_rates_r06.txt, profiles/pmc_valu_r06.json)
+ISSUE_CEILING_TOPS = 256 * 64 * 2.4e9 / 1e12
 
 
 def load_peak():
@@ -77,6 +80,18 @@ def load_ntt_issue():
         with open(os.path.join(ROOT, "profiles", "ntt_issue_r05.json")) as f:
             d = json.load(f)
         return {k: v.get(d.get("current", "cur")) for k, v in d["sizes"].items()}
+    except Exception:
+        return {}
+
+
+def load_valu_counted():
+    """Counted VALU busy per launch kind (profiles/pmc_valu_r06.json, tools/prof/valu_counted.py): the VALU's busy
+    quad-cycles are SQ_INSTS_VALU - SQ_ACTIVE_INST_VALU2 (two full-rate instructions of two waves share one
+    quad-cycle; every other VALU instruction takes one), over 1024 SIMDs x the launch's own clock."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "pmc_valu_r06.json")) as f:
+            d = json.load(f)
+        return {k: v["valu_busy_counted"] for k, v in d["accumulate"].items()}
     except Exception:
         return {}
 
@@ -455,10 +470,14 @@ def accumulate_rooflines(launches, peak, peak_src, traffic):
     if "B2" in kinds:
         lines["B2"] = line(kinds["B2"], 3, "k_accumulate<Fq2>")
     pk = (traffic or {}).get("per_kind", {})
+    busy = load_valu_counted()
     for k, ln in lines.items():  # counted issue share and clock of the same kernel (each launch alone)
-        src = pk.get("H" if k == "H" else ("B2" if k == "B2" else "witness (A, B1, C)"))
+        kk = "H" if k == "H" else ("B2" if k == "B2" else "witness (A, B1, C)")
+        src = pk.get(kk)
         if src:
             ln.update(src)
+        if kk in busy:
+            ln["valu_busy_counted_pmc"] = busy[kk]
         if ln.get("achieved"):
             ln["frac_vs_issue_ceiling"] = round(ln["achieved"] / ISSUE_CEILING_TOPS, 4)
     h = lines.get("H") or {}
@@ -474,9 +493,15 @@ def accumulate_rooflines(launches, peak, peak_src, traffic):
         "algorithmic_work_per_launch": {"mixed_adds": h.get("mixed_adds_per_launch"), "fp_mul_per_add": FPMUL_PER_MADD,
                                         "mac_per_fp_mul": MAC_PER_FPMUL},
         "valu_issue_frac_pmc": traffic.get("valu_issue_frac") if traffic else None,
+        "valu_busy_counted_pmc": busy.get("H"),
+        "valu_busy_note": "valu_issue_frac_pmc prices every VALU instruction at one quad-cycle; valu_busy_counted_pmc "
+                          "subtracts the quad-cycles two waves' full-rate instructions shared (SQ_ACTIVE_INST_VALU2, "
+                          "profiles/pmc_valu_r06.json): 1.6 % of the H launch's instructions",
         "clock_GHz_pmc": traffic.get("clock_GHz") if traffic else None,
         "frac_vs_issue_ceiling": round(h["achieved"] / ISSUE_CEILING_TOPS, 4) if h.get("achieved") else None,
         "issue_ceiling": ISSUE_CEILING_TOPS,
+        "issue_ceiling_note": "one v_mad_u64_u32 per SIMD per quad-cycle (4 clocks, profiles/valu_rates_r06.txt) on "
+                              "1024 SIMDs at 2.4 GHz; full-rate 2-clock ops gain only when two waves co-issue them",
         "traffic_note": "HBM bytes per launch (FETCH x1 + WRITE): ~101 B per mixed addition, 1.49x the per-addition "
                         "minimum (64-B base + 4-B index = 68 B) and 13.7x SURVEY.md §8d's MSM floor (2^23 x 96 B): the "
                         "cost of the 13-row precomputed base table (random gathers over 7 GB; 2.6 L1-TLB misses per "
@@ -627,7 +652,7 @@ def compact_line(out):
     r = out.get("roofline") or {}
     c["roofline"] = {k: r[k] for k in ("kernel", "bound", "achieved", "peak", "unit", "frac", "traffic",
                                       "algorithmic_work_per_launch", "avg_launch_ms", "launches_timed",
-                                      "valu_issue_frac_pmc", "valu_busy_weighted_pmc", "clock_GHz_pmc",
+                                      "valu_issue_frac_pmc", "valu_busy_counted_pmc", "clock_GHz_pmc",
                                       "frac_vs_issue_ceiling", "issue_ceiling", "hbm_GBps", "peak_source")
                      if k in r}
     g2 = (out.get("roofline_launches") or {}).get("roofline_g2")

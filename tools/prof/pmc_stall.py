@@ -54,7 +54,7 @@ def summarize(ds, work=None):
         if work:
             o["valu_lane_instructions_per_unit"] = round(avg["SQ_INSTS_VALU"] * 64 / work, 1)
     if cyc and "SQ_ACTIVE_INST_VALU" in avg:
-        o["active_valu_frac"] = round(avg["SQ_ACTIVE_INST_VALU"] * 4 / (SIMDS * cyc), 4)
+        pass  # SQ_ACTIVE_INST_VALU equals SQ_INSTS_VALU (it counts instructions): not a cycle measure
     wc = avg.get("SQ_WAVE_CYCLES")
     if wc:
         if cyc:
