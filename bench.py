@@ -75,7 +75,7 @@ def load_peak():
 
 def load_ntt_issue():
     """Counted NTT issue figures of the current library (profiles/ntt_issue_r05.json, its "current" entry per size:
-    tools/gpu/r5/pmc.sh, ntt_root1.sh)."""
+    273c6e8:tools/gpu/r5/pmc.sh, ntt_root1.sh)."""
     try:
         with open(os.path.join(ROOT, "profiles", "ntt_issue_r05.json")) as f:
             d = json.load(f)

@@ -1,10 +1,11 @@
-# A/B on one box: bench with abtest/libzkp_amd_base.so (ZKP_LIB_PATH) vs the in-tree library,
-# alternating, N rounds (default 2).  Usage: bash tools/gpu/ab.sh [rounds] [extra bench args]
-set -e
-cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-mkdir -p gpurun_out
+# A/B on one box: the default timing loop with a base library (ZKP_LIB_PATH, built on the CPU into the
+# git-ignored abtest/) against the in-tree library, alternating, N rounds; tools/gpu/ab_summary.py tabulates
+#   bash tools/gpu/ab.sh <tag> [rounds=2] [base .so=abtest/libzkp_amd_base.so] [extra bench args]
+source "$(dirname "$0")/common.sh"
 N=${1:-2}; shift || true
+BASE=${1:-$PWD/abtest/libzkp_amd_base.so}; shift || true
 for i in $(seq 1 $N); do
-  ZKP_LIB_PATH=$PWD/abtest/libzkp_amd_base.so timeout -k 10 300 python bench.py --steps 20 --warmup 3 --cpu-baseline none --batch 0 "$@" > gpurun_out/ab_base_$i.log 2>&1
-  timeout -k 10 300 python bench.py --steps 20 --warmup 3 --cpu-baseline none --batch 0 "$@" > gpurun_out/ab_new_$i.log 2>&1
+  ZKP_LIB_PATH=$BASE timeout -k 10 300 python bench.py --steps 20 --warmup 3 --cpu-baseline none --batch 0 --no-kernels --no-bool0-line --sustain-s 0 "$@" > $O/ab_base_$i.json 2> $O/ab_base_$i.err
+  timeout -k 10 300 python bench.py --steps 20 --warmup 3 --cpu-baseline none --batch 0 --no-kernels --no-bool0-line --sustain-s 0 "$@" > $O/ab_new_$i.json 2> $O/ab_new_$i.err
 done
+echo ab done

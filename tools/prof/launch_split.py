@@ -10,6 +10,9 @@ usage: launch_split.py <kernel_trace.csv> <marker_api_trace.csv> <bench.json> [o
 import csv
 import json
 import sys
+import os as _os, sys as _sys
+_sys.path.insert(0, _os.path.dirname(_os.path.abspath(__file__)))
+import benchline  # noqa: E402
 
 MAC_PER_FPMUL, FPMUL_PER_MADD = 136, 11
 
@@ -30,7 +33,7 @@ def timed_range(marker_csv):
 
 
 def main(trace_csv, marker_csv, bench_json, out=None):
-    line = json.loads(open(bench_json).read().strip().splitlines()[-1])
+    line = benchline.detail(bench_json)
     per_kind = line["roofline_launches"]["per_kind"]
     peak = line["roofline"]["peak"]
     t0, t1 = timed_range(marker_csv)

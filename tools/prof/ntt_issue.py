@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """NTT issue rate per launch kind, from a rocprofv3 kernel trace and a PMC pass of the same
-command (tools/probe/ntt_run.py; tools/gpu/r4/nttpmc.sh): per k_ntt kind, the median launch
+command (tools/probe/ntt_run.py; 273c6e8:tools/gpu/r4/nttpmc.sh): per k_ntt kind, the median launch
 duration, VALU lane-instructions per element and the issue rate (wave-level VALU instructions per
 microsecond per CU), and per coset extension the credited butterfly products per instruction.
 The ratio of the 2^20 and 2^23 rooflines factors into (credited products per instruction) x

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """One library's entry of profiles/ntt_issue_r05.json from the k_ntt rows of one rocprofv3 --pmc pass
-(SQ + GRBM, tools/gpu/r5/pmc.sh / ntt_root1.sh) of `tools/probe/ntt_run.py <k> 20`: per k_ntt mode the
+(SQ + GRBM, 273c6e8:tools/gpu/r5/pmc.sh / ntt_root1.sh) of `tools/probe/ntt_run.py <k> 20`: per k_ntt mode the
 clock, VALU issue and wave-cycle split of tools/prof/pmc_stall.py plus VALU lane-instructions per
 element (SQ_INSTS_VALU x 64 / n); per coset extension 2 x k_ntt<0> + 2 x k_ntt<1> + k_ntt<2>.
 usage: ntt_issue5.py <run_counter_collection.csv> <log_n>"""

@@ -11,10 +11,13 @@ import collections
 import csv
 import json
 import sys
+import os as _os, sys as _sys
+_sys.path.insert(0, _os.path.dirname(_os.path.abspath(__file__)))
+import benchline  # noqa: E402
 
 
 def main(bench_json, out, *files):
-    line = json.loads(open(bench_json).read().strip().splitlines()[-1])
+    line = benchline.detail(bench_json)
     kinds = line["roofline_launches"]["per_kind"]
     h_wg = set(kinds["H"]["workgroups"])
     w_wg = set(kinds["A"]["workgroups"])

@@ -4,7 +4,7 @@ bench.py): for each kind (H, the witness launches A/B1/C, B2) the cycle accounti
 (effective clock from GRBM_GUI_ACTIVE, VALU issue fraction at that clock and at 2.4 GHz, the wave-cycle
 split, lane-instructions per addition) from the SQ pass, HBM bytes per dispatch from the FETCH_SIZE
 (x1: random 64-B gathers, profiles/fetch_calibration_r02.json) and WRITE_SIZE passes, and the L1 TLB
-(UTCL1) miss share from the TCP pass -- all passes of the same bench command (tools/gpu/r5/pmc.sh).
+(UTCL1) miss share from the TCP pass -- all passes of the same bench command (273c6e8:tools/gpu/r5/pmc.sh).
 usage: pmc_launch5.py <pmc dir> <out.json>"""
 import collections
 import csv
@@ -14,10 +14,13 @@ import sys
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 import pmc_stall  # noqa: E402
+import os as _os, sys as _sys
+_sys.path.insert(0, _os.path.dirname(_os.path.abspath(__file__)))
+import benchline  # noqa: E402
 
 
 def per_kind(d, name):
-    bench = json.loads(open(os.path.join(d, name + ".json")).read().strip().splitlines()[-1])
+    bench = benchline.detail(os.path.join(d, name + ".json"))
     kinds = bench["roofline_launches"]["per_kind"]
     hwg, wwg = set(kinds["H"]["workgroups"]), set(kinds["A"]["workgroups"])
     agg = collections.defaultdict(lambda: collections.defaultdict(float))

@@ -21,6 +21,9 @@ import csv
 import json
 import re
 import sys
+import os as _os, sys as _sys
+_sys.path.insert(0, _os.path.dirname(_os.path.abspath(__file__)))
+import benchline  # noqa: E402
 
 SIMDS = 1024
 MAXCLK_GHZ = 2.4
@@ -66,7 +69,7 @@ def summarize(ds, work=None):
 
 
 def acc(bench_json, path, out=None):
-    line = json.loads(open(bench_json).read().strip().splitlines()[-1])
+    line = benchline.detail(bench_json)
     kinds = line["roofline_launches"]["per_kind"]
     h_wg = set(kinds["H"]["workgroups"])
     w_wg = set(kinds["A"]["workgroups"])

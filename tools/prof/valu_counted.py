@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Counted VALU busy from one rocprofv3 --pmc pass per workload with SQ_INSTS_VALU,
 SQ_ACTIVE_INST_VALU2, SQ_INSTS_VALU_INT32, SQ_INSTS_VALU_INT64, SQ_ACTIVE_INST_VALU, SQ_THREAD_CYCLES_VALU,
-SQ_WAVES, SQ_WAVE_CYCLES and GRBM_GUI_ACTIVE (tools/gpu/r6/valu.sh; raw rows in profiles/pmc_valu_r06/).
+SQ_WAVES, SQ_WAVE_CYCLES and GRBM_GUI_ACTIVE (tools/gpu/pmc.sh valu ntt + ubench.sh valu_rates (the round-6 call: f1362da:tools/gpu/r6/valu.sh); raw rows in profiles/pmc_valu_r06/).
 
 The round-5 issue model priced every VALU instruction at one quad-cycle (4 clocks) of its SIMD.  gfx950
 executes the full-rate class (v_and/or/xor/add/sub/mov/lshrrev_b32 ... e32, v_bitop3) in 2 clocks, but a
@@ -56,7 +56,7 @@ def line(ds, work=None):
 
 
 def summarise():
-    res = {"source": "profiles/pmc_valu_r06/ (tools/gpu/r6/valu.sh)", "opcodes_alone": {}, "accumulate": {},
+    res = {"source": "profiles/pmc_valu_r06/ (tools/gpu/pmc.sh valu ntt + ubench.sh valu_rates (the round-6 call: f1362da:tools/gpu/r6/valu.sh))", "opcodes_alone": {}, "accumulate": {},
            "ntt": {}}
     for d in dispatches("ub_counter_collection.csv"):
         op = re.sub(r"^k_", "", d["name"].split("(")[0])

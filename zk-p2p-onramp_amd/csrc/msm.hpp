@@ -84,7 +84,7 @@ struct MsmParams {
 // digits fall into a handful of buckets, i.e. into one or a few sub-bins of the sort's pass C,
 // which gives every sub-bin ONE workgroup -- measured 1.3 ms for that kernel alone at 2^20
 // points and c = 18 (0.05 ms at c = 20), +13 ms per Venmo proof at c = 21
-// (tools/gpu/experiments/r2_hsort_c*.sh).  Keep c whose top window spans >= 12 bits (>= 128
+// (273c6e8:tools/gpu/experiments/r2_hsort_c*.sh).  Keep c whose top window spans >= 12 bits (>= 128
 // sub-bins), trying c+1, c-1, c+2, ... within [8, 20]; below 2^17 points one workgroup per
 // sub-bin copes (n entries at most), so c stays.
 inline int dense_window_bits(int c, size_t n) {

@@ -197,7 +197,7 @@ static MsmParams make_params(size_t n, int c, int depth) {
 // (one bucket set) unless the tables would not fit in half of the free HBM, then the largest depth
 // that does (ZKP_MSM depth= overrides).
 static void choose_msm_params(size_t n_w, size_t n_h, const MsmOptions& o, MsmParams& pw, MsmParams& ph) {
-  // measured on the Venmo shape (tools/gpu/experiments/sweep_c2.sh): the witness MSMs (70 % of the
+  // measured on the Venmo shape (273c6e8:tools/gpu/experiments/sweep_c2.sh): the witness MSMs (70 % of the
   // digits of a 0/1-heavy witness are single entries) prefer one bit less than lg n - 4, the
   // uniform-scalar H MSM one bit more (fewer windows; the bucket reduction is cheap), moved off the
   // widths whose top window collapses into a few buckets (dense_window_bits)
@@ -1581,7 +1581,7 @@ struct MsmRig {
     try {
       // automatic window bits and plan: the prover's H-MSM choice (dense plan, c = lg n - 3 clamped to
       // [8, 20] and moved off a collapsed top window); measured on configs[1] (G1 2^20, uniform
-      // scalars, tools/gpu/experiments/r2_msm_c.sh): 1.84 ms against 2.06 ms for a compacted plan at
+      // scalars, 273c6e8:tools/gpu/experiments/r2_msm_c.sh): 1.84 ms against 2.06 ms for a compacted plan at
       // c = lg n - 4.  ZKP_MSM plan=compact selects the witness plan's variant (tests).
       int lg = 0;
       while ((size_t(1) << lg) < n) ++lg;
