@@ -122,6 +122,9 @@ def main(n=300):
     quads4 = [[rnd.randrange(3 * R) for _ in range(4)] for _ in range(n)]
     quads4 += [[a, b, c, d] for a in x3e for b in x3e for c in x3e[2:4] for d in x3e[2:4]]
     quads4 += [[a, b, c, d] for a in x3e[2:4] for b in x3e[2:4] for c in x3e for d in x3e]
+    # a small s02 against a maximal s13 (the top limb of s02 - s13 + 6m wrapped below zero)
+    quads4 += [[a, b, c, d] for a in (0, 1) for c in (0, 1) for b in x3e[2:4] for d in x3e[2:4]]
+    quads4 += [[b, a, d, c] for a in (0, 1) for c in (0, 1) for b in x3e[2:4] for d in x3e[2:4]]
     for k, (x0, x1, x2, x3) in enumerate(quads4):
         wv = R - 1 if k % 3 == 0 else rnd.randrange(R)
         tw = twe[k % 3] if k % 2 == 0 else rnd.randrange(2 * R)

@@ -663,17 +663,19 @@ ZDEV Fe<C> sub_raw6(const Fe<C>& a, const Fe<C>& b) {
   return s;
 }
 
-// a - b + 6m for raw sums a, b < 6m of two normalised values each (limbs < 2^30), WITHOUT a carry
-// pass: the 6m borrow form whose low limbs are raised by 2^30 (consts MOD6_B30) keeps every limb
-// >= 0 and < 2^30 + 2^30 + 2^29 = 2.5 * 2^30, value < 12m.  An operand of mul_shoup (column sums
+// a - b + 8m for raw sums a, b < 6m of two normalised values each (limbs < 2^30), WITHOUT a carry
+// pass: the 8m borrow form whose low limbs are raised by 2^30 (consts MOD8_B30) keeps every limb
+// >= 0 and < 2^30 + 2^30 + 2^29 = 2.5 * 2^30, value < 14m.  An operand of mul_shoup (column sums
 // <= 9 (2.5 + 0.5) 2^59 < 2^63.8), of mul() against a normalised value, or of qreduce (limbs
 // < 2^32 - 2^10) -- never a second raw operand (the NTT's radix-4 unit, round 5: 24 instructions
-// fewer than sub_raw6 per use)
+// fewer than sub_raw6 per use).  The top limb: b's is at most 2 x (3m - 1)'s (0x12259d6), and 8m's
+// raised form keeps 0x1832270 there, so it stays >= 0 for every a (round 6, ADVICE r5: the 6m form's
+// 0x12259d4 wrapped below zero for a ~ 0 against b ~ 6m; tools/hosttest r4lazy covers that quad)
 template <class C>
 ZDEV Fe<C> sub_raw6n(const Fe<C>& a, const Fe<C>& b) {
   Fe<C> s;
 #pragma unroll
-  for (int i = 0; i < NL; ++i) s.v[i] = a.v[i] + C::MOD6_B30[i] - b.v[i];
+  for (int i = 0; i < NL; ++i) s.v[i] = a.v[i] + C::MOD8_B30[i] - b.v[i];
   return s;
 }
 

@@ -371,6 +371,11 @@ class DevicePipeline {
         ws_[k].pw = o.pw, ws_[k].ta = o.ta, ws_[k].tb1 = o.tb1, ws_[k].tc = o.tc, ws_[k].tb2 = o.tb2;
       }
       th_ = share->th_;
+      // the H plan and engine must read th_ with the parameters it was built with: a sibling's own
+      // choose_msm_params can pick another depth when less HBM is free by now
+      ph = share->plan_h_->params();
+      if (th_->c() != ph.c || th_->depth() != ph.depth)
+        throw ZkpError(ZKP_ERR_INTERNAL, "shared H table built with other parameters");
     } else {
       ws_[0].pw = pw;
       build_wtables(ws_[0]);
@@ -439,6 +444,10 @@ class DevicePipeline {
     }
     HIPX(hipMalloc(&dwin_, win_total() * 4));
     HIPX(hipHostMalloc(&hwin_, win_total() * 4, hipHostMallocDefault));
+    // a full prover's first upload slot exists from load on, so a one-shot prover's first host-witness
+    // proof does not pay its ~410 MB of HBM, ~220 MB of pinned memory, streams and copy threads, and an
+    // out-of-memory surfaces here rather than at prove time; the second slot stays lazy
+    if (nparts == 1) ensure_upload_slot(0);
     HIPX(hipStreamSynchronize(s0_));
   }
 

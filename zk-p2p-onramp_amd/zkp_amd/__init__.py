@@ -767,8 +767,13 @@ def bench_msm(points_lem: bytes, scalars_le: bytes, g2: bool = False, warmup: in
     st = (ctypes.c_double * 8)()
     out = (ctypes.c_uint8 * 128)()
     inf = ctypes.c_int()
-    _check(lib.zkp_bench_msm_ex(device, 1 if g2 else 0, pp, sp, n, warmup, iters, st, 8,
-                                ctypes.cast(out, ctypes.POINTER(ctypes.c_uint8)), ctypes.byref(inf)))
+    ext = hasattr(lib, "zkp_bench_msm_ex")  # an older library (A/B runs) has the 6-stat form only
+    if ext:
+        _check(lib.zkp_bench_msm_ex(device, 1 if g2 else 0, pp, sp, n, warmup, iters, st, 8,
+                                    ctypes.cast(out, ctypes.POINTER(ctypes.c_uint8)), ctypes.byref(inf)))
+    else:
+        _check(lib.zkp_bench_msm(device, 1 if g2 else 0, pp, sp, n, warmup, iters, st,
+                                 ctypes.cast(out, ctypes.POINTER(ctypes.c_uint8)), ctypes.byref(inf)))
     raw = bytes(out)
     if inf.value:
         res = None
@@ -778,7 +783,8 @@ def bench_msm(points_lem: bytes, scalars_le: bytes, g2: bool = False, warmup: in
     else:
         res = (_le(raw[:32]), _le(raw[32:64]))
     stats = {"ms_per_msm": st[0], "ms_accumulate": st[1], "mixed_adds": int(st[2]), "tasks": int(st[3]),
-             "c": int(st[4]), "windows": int(st[5]), "table_build_ms": st[6], "table_depth": int(st[7])}
+             "c": int(st[4]), "windows": int(st[5]), "table_build_ms": st[6] if ext else None,
+             "table_depth": int(st[7]) if ext else None}
     return stats, res
 
 
