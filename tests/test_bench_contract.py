@@ -12,7 +12,7 @@ import pathlib
 import pytest
 
 PROFILES = pathlib.Path(__file__).resolve().parent.parent / "profiles"
-LINES = ["bench_r01.json", "bench_r01_recheck.json", "bench_r05_final.json", "bench_r06_a.json"]
+LINES = ["bench_r01.json", "bench_r01_recheck.json", "bench_r05_final.json", "bench_r06_a.json", "bench_r06_b.json"]
 REQUIRED = ["metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
             "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"]
 
@@ -100,7 +100,7 @@ def test_round6_compact_line():
     stays below 6,000 bytes and carries both halves of the metric (proofs/s and the 1-proof latency), the
     verified batch, the sustained >= 30-s rate, the roofline and cpu_baseline; the detail object is the
     line before it."""
-    path = PROFILES / "bench_r06_a.json"
+    path = PROFILES / "bench_r06_b.json"
     if not path.exists():
         pytest.skip("bench_r06_a.json not committed")
     lines = path.read_text().strip().splitlines()

@@ -57,3 +57,14 @@ def test_ntt_2_20_edge_values(co):
         got = zkp_amd.ntt_fr_bytes(raw, mode)
         want = co.ntt(raw, mode, threads=THREADS)
         assert got == want, (mode, _first_diff(got, want))
+
+
+@pytest.mark.parametrize("k", [16, 18, 19, 21, 22])
+def test_ntt_other_sizes_full_vector(co, k):
+    """Every pass split between the pinned sizes (16 = 8+8, 18 = 6+6+6, 19 = 7+6+6, 21 = 7+7+7, 22 = 8+7+7):
+    the three transforms full-vector against the C++ oracle on a SplitMix stream of their own."""
+    raw = synth.scalars(SEED + k, 2, 1 << k)
+    for mode in (0, 1, 2):
+        got = zkp_amd.ntt_fr_bytes(raw, mode)
+        want = co.ntt(raw, mode, threads=THREADS)
+        assert got == want, (mode, _first_diff(got, want))
