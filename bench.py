@@ -102,7 +102,10 @@ def load_traffic():
     bytes exactly (profiles/fetch_calibration_r02.json; the x2 of coalesced 16-B streams does not
     apply).  Round 4's summary is per launch kind (the H launch, the roofline's); older summaries
     averaged every G1 launch and are recomputed from their raw counters."""
-    p = os.path.join(ROOT, "profiles", "pmc_launch_r05.json")
+    for name in ("pmc_launch_r06.json", "pmc_launch_r05.json"):
+        p = os.path.join(ROOT, "profiles", name)
+        if os.path.exists(p):
+            break
     try:
         with open(p) as f:
             d = json.load(f)
@@ -114,9 +117,9 @@ def load_traffic():
                                  "valu_lane_instructions_per_addition_pmc": v["valu_lane_instructions_per_addition"],
                                  "hbm_bytes_per_addition_pmc": v.get("hbm_bytes_per_addition")}
                              for k, v in d["kinds"].items()},
-                "source": "profiles/pmc_launch_r05.json (the H launch: rocprofv3 --pmc FETCH_SIZE x1 + WRITE_SIZE, "
+                "source": "profiles/%s (the H launch: rocprofv3 --pmc FETCH_SIZE x1 + WRITE_SIZE, "
                           "gather-calibrated; SQ_INSTS_VALU and GRBM_GUI_ACTIVE: issue share at the launch's own clock; "
-                          "tools/prof/pmc_launch5.py)"}
+                          "tools/prof/pmc_launch5.py)" % name}
     except Exception:
         pass
     p = os.path.join(ROOT, "profiles", "pmc_launch_r04.json")

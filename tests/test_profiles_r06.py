@@ -57,3 +57,35 @@ def test_valu_counted_findings():
     assert h["valu_issue_frac_4cyc"] - h["valu_busy_counted"] < 0.02 and h["valu_busy_counted"] > 0.92
     assert h["valu_busy_counted"] == pytest.approx(
         h["valu_issue_frac_4cyc"] * (1 - h["dual_issue_quad_cycles_per_instr"]), abs=2e-4)
+
+
+P = os.path.join(ROOT, "profiles")
+
+
+def test_launch_split_r06_reproduces_bench_fracs(tmp_path):
+    """The round-6 kernel trace (k_accumulate rows + the ROCTx "bench timed" range of the same bench
+    invocation, tools/gpu/trace.sh) recomputes every launch kind's frac of profiles/bench_r06_rocprof_run.json
+    within 0.01, and the committed launch_split_r06.json is that output."""
+    out = tmp_path / "split.json"
+    subprocess.run([sys.executable, os.path.join(ROOT, "tools", "prof", "launch_split.py"),
+                    os.path.join(P, "rocprof_r06_accumulate_trace.csv"), os.path.join(P, "rocprof_r06_marker_trace.csv"),
+                    os.path.join(P, "bench_r06_rocprof_run.json"), str(out)], check=True, capture_output=True, timeout=120)
+    res = json.loads(out.read_text())
+    assert set(res["kinds"]) == {"A", "B1", "C", "H", "B2"}
+    for kind, v in res["kinds"].items():
+        assert v["dispatches"] == v["bench_launches"], kind
+        assert abs(v["frac_delta"]) <= 0.01, (kind, v)
+    assert res["kinds"] == json.load(open(os.path.join(P, "launch_split_r06.json")))["kinds"]
+
+
+def test_pmc_launch_r06_recomputes(tmp_path):
+    """profiles/pmc_launch_r06.json (what bench.py's roofline `traffic`, issue share and clock read) from the
+    committed k_accumulate rows of the round-6 SQ / FETCH_SIZE / WRITE_SIZE passes (tools/gpu/pmc.sh)."""
+    out = tmp_path / "pmc.json"
+    subprocess.run([sys.executable, os.path.join(ROOT, "tools", "prof", "pmc_launch5.py"),
+                    os.path.join(P, "pmc_launch_r06"), str(out), "x"], check=True, capture_output=True, timeout=120)
+    got = json.loads(out.read_text())
+    want = json.load(open(os.path.join(P, "pmc_launch_r06.json")))
+    assert got["kinds"] == want["kinds"]
+    h = got["kinds"]["H"]
+    assert h["valu_issue_frac"] > 0.9 and 1.3 < h["hbm_bytes_per_addition"] / 68 < 1.6

@@ -36,16 +36,17 @@ def per_kind(d, name):
     return {k: {c: v / len(disp[k]) for c, v in agg[k].items()} for k in agg}
 
 
-def main(d, out):
+def main(d, out, source=None):
     import io
     import contextlib
     with contextlib.redirect_stdout(io.StringIO()):
         pmc_stall.acc(os.path.join(d, "sq.json"), os.path.join(d, "sq", "run_counter_collection.csv"), "/tmp/_sq.json")
     sq = json.load(open("/tmp/_sq.json"))["kinds"]
-    fetch, write, tcp = per_kind(d, "fetch"), per_kind(d, "write"), per_kind(d, "tcp")
-    res = {"source": "rocprofv3 --pmc passes of `bench.py --steps 4 --warmup 1 --batch 0 --no-kernels --no-bool0-line` "
-                     "(tools/gpu/r5/pmc.sh): SQ+GRBM; FETCH_SIZE; WRITE_SIZE + TCC_HIT_sum; TCP UTCL1; "
-                     "split per launch kind by tools/prof/pmc_launch5.py",
+    fetch, write = per_kind(d, "fetch"), per_kind(d, "write")
+    tcp = per_kind(d, "tcp") if os.path.isdir(os.path.join(d, "tcp")) else {}
+    res = {"source": source or ("rocprofv3 --pmc passes of `bench.py --steps 4 --warmup 1 --batch 0 --no-kernels "
+                                "--no-bool0-line` (tools/gpu/r5/pmc.sh): SQ+GRBM; FETCH_SIZE; WRITE_SIZE + TCC_HIT_sum; "
+                                "TCP UTCL1; split per launch kind by tools/prof/pmc_launch5.py"),
            "kinds": {}}
     for k, label in (("H", "H"), ("W", "witness (A, B1, C)"), ("B2", "B2")):
         s = sq[label]
@@ -75,4 +76,4 @@ def main(d, out):
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:3])
+    main(*sys.argv[1:4])
