@@ -8,9 +8,10 @@
 // Key bits kb = ceil(log2 buckets) split as b1 (bin) + b2 (sub-bin) + b3 (bucket in sub-bin);
 // for the Venmo H plan (2^19 buckets) 7 + 7 + 5; b3 grows past 5 (tiled pass C) only for kb > 23.  Three MSD passes, every scatter staged in LDS
 // so that consecutive lanes write consecutive addresses of one destination run:
-//   A  k_hs_count1 / k_hs_binscan / k_hs_binbase / k_hs_scatter1
+//   A  k_hs_count1 / scan / k_hs_binbase / k_hs_scatter1
 //        digits computed from the scalars (zero digits dropped), grouped by bin: per (bin, block
-//        of K * HS_TPB scalars, <= HS_STAGE entries) counts, per-bin block offsets, bin bases; a
+//        of K * HS_TPB scalars, <= HS_STAGE entries) counts, their bin-major exclusive scan (every
+//        (bin, block) run's position), bin bases; a
 //        block's entries counted, scanned and placed in LDS, then written as runs (~52 entries
 //        per bin for 2^7 bins), entries (key, base|sign) as one 8-byte word
 //   B  k_hs_count2 / scan / k_hs_subbase / k_hs_scatter2
@@ -221,34 +222,26 @@ __global__ __launch_bounds__(HS_TPB) void k_hs_count1(const uint32_t* __restrict
   for (uint32_t b = threadIdx.x; b < nbins; b += HS_TPB) hist[(size_t)b * gridDim.x + blockIdx.x] = h[b];
 }
 
-// one workgroup per bin: hist[bin][blk] -> exclusive block offsets inside the bin, bin total
-__global__ __launch_bounds__(HS_TPB) void k_hs_binscan(const uint32_t* __restrict__ hist, uint32_t nblk,
-                                                       uint32_t* __restrict__ blkoff, uint32_t* __restrict__ bintot) {
-  __shared__ uint32_t sh[HS_TPB / 64];
-  const size_t row = (size_t)blockIdx.x * nblk;
-  uint32_t carry = 0;
-  for (uint32_t j0 = 0; j0 < nblk; j0 += HS_TPB) {
-    const uint32_t j = j0 + threadIdx.x;
-    const uint32_t v = j < nblk ? hist[row + j] : 0u;
-    uint32_t tot;
-    const uint32_t e = block_excl_scan<HS_TPB>(v, sh, tot);
-    if (j < nblk) blkoff[row + j] = carry + e;
-    carry += tot;
-  }
-  if (threadIdx.x == 0) bintot[blockIdx.x] = carry;
-}
-
-// bin bases and pass-B tile offsets (nbins <= 512, one workgroup):
-//   binbase[b] = entries of bins < b (binbase[nbins] = all), toff[b] = tiles of bins < b
-__global__ __launch_bounds__(512) void k_hs_binbase(const uint32_t* __restrict__ bintot, uint32_t nbins,
-                                                    uint32_t* __restrict__ binbase, uint32_t* __restrict__ toff) {
+// bin bases and pass-B tile offsets from the exclusive scan of the whole bin-major hist[bin][blk] array
+// (nbins <= 512, one workgroup): that scan IS every (bin, block) run's final position (bin base + the
+// block's offset inside its bin), so a look-back-free device scan (3 full-width launches) replaces the
+// per-bin sequential scan that one workgroup per bin did over ~16 K blocks (0.3 ms on the H plan's
+// critical path, round 6):  binbase[b] = entries of bins < b (binbase[nbins] = all), toff[b] = tiles of
+// bins < b
+__global__ __launch_bounds__(512) void k_hs_binbase(const uint32_t* __restrict__ pos, const uint32_t* __restrict__ hist,
+                                                    uint32_t nbins, uint32_t nblk, uint32_t* __restrict__ binbase,
+                                                    uint32_t* __restrict__ toff) {
   __shared__ uint32_t sh[512 / 64];
-  const uint32_t v = threadIdx.x < nbins ? bintot[threadIdx.x] : 0u;
-  uint32_t tot, ttot;
-  const uint32_t e = block_excl_scan<512>(v, sh, tot);
+  const size_t last = (size_t)nbins * nblk - 1;
+  const uint32_t all = pos[last] + hist[last];
+  const uint32_t b = threadIdx.x;
+  const uint32_t lo = b < nbins ? pos[(size_t)b * nblk] : all;
+  const uint32_t hi = b + 1 < nbins ? pos[(size_t)(b + 1) * nblk] : all;
+  const uint32_t v = b < nbins ? hi - lo : 0u;
+  uint32_t ttot;
   const uint32_t te = block_excl_scan<512>((v + HS_TILE - 1) / HS_TILE, sh, ttot);
-  if (threadIdx.x < nbins) binbase[threadIdx.x] = e, toff[threadIdx.x] = te;
-  if (threadIdx.x == 0) binbase[nbins] = tot, toff[nbins] = ttot;
+  if (b < nbins) binbase[b] = lo, toff[b] = te;
+  if (b == 0) binbase[nbins] = all, toff[nbins] = ttot;
 }
 
 // the block's digits counted per bin, scanned, placed in an LDS stage grouped by bin (LDS
@@ -256,8 +249,7 @@ __global__ __launch_bounds__(512) void k_hs_binbase(const uint32_t* __restrict__
 template <int K>
 __global__ __launch_bounds__(HS_TPB) void k_hs_scatter1(const uint32_t* __restrict__ scalars, uint32_t n, int c,
                                                         int W, int T, int sh1, uint32_t nbins,
-                                                        const uint32_t* __restrict__ blkoff,
-                                                        const uint32_t* __restrict__ binbase,
+                                                        const uint32_t* __restrict__ pos,
                                                         uint2* __restrict__ ent) {
   constexpr int NB = 1 << HS_MAX_B1;
   // dynamic LDS: the stage (K * HS_TPB * W entries) then cnt / off (nbins each): 54.3 KiB for the
@@ -304,7 +296,7 @@ __global__ __launch_bounds__(HS_TPB) void k_hs_scatter1(const uint32_t* __restri
       if (e[q][w].x != NONE) stage[atomicAdd(&cnt[e[q][w].x >> sh1], 1u)] = e[q][w];
   __syncthreads();
   for (uint32_t b = threadIdx.x; b < nbins; b += HS_TPB)  // the cursors become destination bases
-    off[b] = binbase[b] + blkoff[(size_t)b * gridDim.x + blockIdx.x] - off[b];
+    off[b] = pos[(size_t)b * gridDim.x + blockIdx.x] - off[b];
   __syncthreads();
   for (uint32_t j = threadIdx.x; j < total; j += HS_TPB) {
     const uint2 e = stage[j];

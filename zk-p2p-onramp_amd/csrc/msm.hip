@@ -284,7 +284,6 @@ MsmPlan::MsmPlan(size_t max_n, const MsmParams& prm, hipStream_t stream) : MsmPl
   const size_t nh = (size_t)hs_nbins_ * hs_nblk_, nh2 = (size_t)hs_max_tiles_ << hs_b2_;
   HIPX(hipMalloc(&hs_hist_, nh * 4));
   HIPX(hipMalloc(&hs_blkoff_, nh * 4));
-  HIPX(hipMalloc(&hs_bintot_, (hs_nbins_ + 1) * 4));
   HIPX(hipMalloc(&hs_binbase_, (hs_nbins_ + 1) * 4));
   HIPX(hipMalloc(&hs_toff_, (hs_nbins_ + 1) * 4));
   HIPX(hipMalloc(&hs_hist2_, nh2 * 4));
@@ -292,7 +291,7 @@ MsmPlan::MsmPlan(size_t max_n, const MsmParams& prm, hipStream_t stream) : MsmPl
   HIPX(hipMalloc(&hs_subbase_, ((size_t)nq + 1) * 4));
   HIPX(hipMalloc(&hs_ent_a_, max_entries_ * 8));
   HIPX(hipMalloc(&hs_ent_b_, max_entries_ * 8));
-  const size_t scan_n = std::max(std::max(nbuckets_ + 1, nh3), std::max(nh2, ntl));
+  const size_t scan_n = std::max(std::max(std::max(nbuckets_ + 1, nh3), std::max(nh2, ntl)), nh);
   HIPX(hipMalloc(&tsum_, (scan_tiles_for(scan_n) + 1) * 4));
   HIPX(hipEventCreateWithFlags(&ready_, hipEventDisableTiming));
 }
@@ -300,7 +299,7 @@ MsmPlan::MsmPlan(size_t max_n, const MsmParams& prm, hipStream_t stream) : MsmPl
 MsmPlan::~MsmPlan() {
   if (ready_) (void)hipEventDestroy(ready_);
   for (void* p : {(void*)vals_sorted_, (void*)bstart_, (void*)bend_, (void*)cnt_, (void*)off_task_, (void*)hs_hist_,
-                  (void*)hs_blkoff_, (void*)hs_bintot_, (void*)hs_binbase_, (void*)hs_toff_, (void*)hs_hist2_,
+                  (void*)hs_blkoff_, (void*)hs_binbase_, (void*)hs_toff_, (void*)hs_hist2_,
                   (void*)hs_off2_, (void*)hs_subbase_, hs_ent_a_, hs_ent_b_, (void*)tsum_, (void*)perm_,
                   (void*)tl_hist_, (void*)tl_off_, (void*)hs_toff3_, (void*)hs_hist3_, (void*)hs_off3_,
                   (void*)lvl_all_, (void*)lvl_tsum_})
@@ -336,12 +335,13 @@ void MsmPlan::build(const uint32_t* scalars, size_t n) {
     auto count1 = k == 4 ? k_hs_count1<4> : (k == 2 ? k_hs_count1<2> : k_hs_count1<1>);
     hipLaunchKernelGGL(count1, dim3(nblk), dim3(HS_TPB), 0, st, scalars, (uint32_t)n, prm_.c, (int)W, prm_.depth, sh1,
                        hs_nbins_, hs_hist_);
-    hipLaunchKernelGGL(k_hs_binscan, dim3(hs_nbins_), dim3(HS_TPB), 0, st, hs_hist_, nblk, hs_blkoff_, hs_bintot_);
-    hipLaunchKernelGGL(k_hs_binbase, dim3(1), dim3(512), 0, st, hs_bintot_, hs_nbins_, hs_binbase_, hs_toff_);
+    scan_nolookback(hs_hist_, hs_blkoff_, (size_t)hs_nbins_ * nblk, tsum_, st);
+    hipLaunchKernelGGL(k_hs_binbase, dim3(1), dim3(512), 0, st, hs_blkoff_, hs_hist_, hs_nbins_, nblk, hs_binbase_,
+                       hs_toff_);
     auto scatter1 = k == 4 ? k_hs_scatter1<4> : (k == 2 ? k_hs_scatter1<2> : k_hs_scatter1<1>);
     const size_t lds1 = (size_t)k * HS_TPB * W * 8 + (size_t)hs_nbins_ * 8;
     hipLaunchKernelGGL(scatter1, dim3(nblk), dim3(HS_TPB), lds1, st, scalars, (uint32_t)n, prm_.c, (int)W, prm_.depth,
-                       sh1, hs_nbins_, hs_blkoff_, hs_binbase_, ea);
+                       sh1, hs_nbins_, hs_blkoff_, ea);
     // B: bins -> sub-bins (tiles past the used ones exit; their counters stay zero)
     const size_t tiles = ((size_t)total_ + HS_TILE - 1) / HS_TILE + hs_nbins_;
     const size_t nh2 = tiles << hs_b2_;

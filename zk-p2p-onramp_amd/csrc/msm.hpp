@@ -190,7 +190,7 @@ class MsmPlan {
   uint32_t *hs_toff3_ = nullptr, *hs_hist3_ = nullptr, *hs_off3_ = nullptr;
   int hs_b2_ = 0, hs_b3_ = 0, hs_k_ = 1;  // hs_k_: scalars per thread in pass A
   uint32_t hs_nbins_ = 0, hs_nblk_ = 0, hs_max_tiles_ = 0;
-  uint32_t *hs_hist_ = nullptr, *hs_blkoff_ = nullptr, *hs_bintot_ = nullptr, *hs_binbase_ = nullptr;
+  uint32_t *hs_hist_ = nullptr, *hs_blkoff_ = nullptr, *hs_binbase_ = nullptr;
   uint32_t *hs_toff_ = nullptr, *hs_hist2_ = nullptr, *hs_off2_ = nullptr, *hs_subbase_ = nullptr;
   void *hs_ent_a_ = nullptr, *hs_ent_b_ = nullptr;  // 8-byte (key, base|sign) entries
   // accumulate-task order by length (longest first)
