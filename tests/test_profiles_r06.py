@@ -89,3 +89,22 @@ def test_pmc_launch_r06_recomputes(tmp_path):
     assert got["kinds"] == want["kinds"]
     h = got["kinds"]["H"]
     assert h["valu_issue_frac"] > 0.9 and 1.3 < h["hbm_bytes_per_addition"] / 68 < 1.6
+
+
+def test_proof_valu_r06_recomputes(tmp_path):
+    """profiles/proof_valu_r06.json (a proof's VALU work against its span) from the committed
+    per-dispatch counters of three whole proofs: the classes' instruction shares sum to 1, the G1
+    accumulations are the largest share, and the VALU work fills most of the bench's ms per proof."""
+    out = tmp_path / "pv.json"
+    subprocess.run([sys.executable, os.path.join(ROOT, "tools", "prof", "proof_valu.py"),
+                    os.path.join(ROOT, "profiles", "proof_valu_r06", "valu_counter_collection.csv"),
+                    os.path.join(ROOT, "profiles", "bench_r06_c.json"), str(out)],
+                   check=True, capture_output=True, timeout=120)
+    got = json.load(open(out))
+    want = json.load(open(os.path.join(ROOT, "profiles", "proof_valu_r06.json")))
+    for k in ("classes", "valu_busy_simd_cycles_per_proof", "t_valu_ms", "span_filled_by_valu_work", "proofs"):
+        assert got[k] == want[k], k
+    assert got["proofs"] == 3
+    assert abs(sum(c["valu_instr_share"] for c in got["classes"].values()) - 1) < 1e-3
+    assert max(got["classes"], key=lambda k: got["classes"][k]["valu_instr_share"]) == "accumulate G1"
+    assert 0.8 < got["span_filled_by_valu_work"]["2.0 GHz"] < 1.0
