@@ -603,7 +603,23 @@ def sustained_line(args, prover, ndev, nw, refs, dist, sync, on_devices, r_fix, 
             if pr != refs[i % nw]:
                 bad.append((d, i))
             i += 1
-        counts[d] = i
+            counts[d] = i
+    # proofs per window of ~sustain_s / 10 (at most 30 s), printed to stderr as it goes: a long run shows
+    # progress, and the windows show whether the rate drifts (clock, heat) over the run
+    wlen = min(30.0, max(1.0, args.sustain_s / 10))
+    windows = []
+
+    def monitor():
+        last_n, last_t = 0, time.perf_counter()
+        while not stop[0]:
+            time.sleep(0.25)
+            now = time.perf_counter()
+            if now - last_t >= wlen and not stop[0]:
+                n_now = sum(counts)
+                windows.append(round((n_now - last_n) / (now - last_t), 2))
+                print("sustain: %.0f s, %d proofs, %.2f proofs/s in the last window"
+                      % (now - t0, n_now, windows[-1]), file=sys.stderr, flush=True)
+                last_n, last_t = n_now, now
     if dist:
         dist.barrier()
     sync()
@@ -611,10 +627,14 @@ def sustained_line(args, prover, ndev, nw, refs, dist, sync, on_devices, r_fix, 
     timer = threading.Timer(args.sustain_s, lambda: stop.__setitem__(0, True))
     t0 = time.perf_counter()
     timer.start()
+    mon = threading.Thread(target=monitor, daemon=True)
+    mon.start()
     on_devices(loop)
     sync()
     el = time.perf_counter() - t0
     timer.cancel()
+    stop[0] = True
+    mon.join()
     n = sum(counts)
     if dist:
         import torch
@@ -626,7 +646,7 @@ def sustained_line(args, prover, ndev, nw, refs, dist, sync, on_devices, r_fix, 
         n = int(t.item())
     return {"proofs_per_s": round(n / el, 3), "proofs": n, "seconds": round(el, 2),
             "ms_per_proof": round(el / max(1, n) * 1e3 * ndev, 3), "all_proofs_ok": not bad,
-            "mismatched_proofs": bad[:8],
+            "mismatched_proofs": bad[:8], "window_s": wlen, "window_proofs_per_s": windows,
             "note": "staged loop, one proof at a time per device, for >= %.0f s; every proof checked" % args.sustain_s}
 
 
