@@ -128,7 +128,7 @@ static int env_int(const char* name, int dflt) {
 
 // MSM tuning options: ONE environment variable read when a prover (or a kernel-level MSM) is built,
 // ZKP_MSM = "key=value[,key=value...]" (empty / unset: automatic everything):
-//   w=<bits>  h=<bits>    window bits of the witness plan / the H plan (8..24)
+//   w=<bits>  h=<bits>    window bits of the witness plan / the H plan and the kernel-level MSMs (8..24)
 //   depth=<rows>          base-table rows T per point (1..W; default W, or the largest depth whose
 //                         tables fit half of the free HBM)
 //   task_w=<n> task_h=<n> entries per bucket-accumulation task of either plan (default 32 / 48)
@@ -1595,7 +1595,7 @@ struct MsmRig {
       int lg = 0;
       while ((size_t(1) << lg) < n) ++lg;
       const MsmOptions opt = msm_options();
-      const int c_auto = dense_window_bits(std::min(20, std::max(8, lg - 3)), n);
+      const int c_auto = opt.h ? opt.h : dense_window_bits(std::min(20, std::max(8, lg - 3)), n);
       prm = make_params(std::max<size_t>(n, 1), c ? c : c_auto, depth);
       prm.S = opt.task_h > 0 ? opt.task_h : 48;  // the H plan's task size too (choose_msm_params)
       bases = std::make_unique<MsmBases>(curve, n, prm.c, prm.depth);
