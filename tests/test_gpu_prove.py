@@ -34,10 +34,11 @@ def test_prove_bit_exact(golden_dir, name):
 
 # MSM tuning options (ZKP_MSM, read when the prover is built) and the serial profiling mode: other
 # window bits and table depths (several bucket groups folded by Horner), task sizes, bucket-reduction
-# segment sizes, every kernel alone on the device -- every variant must give the same golden proof
+# segment sizes, every kernel alone on the device, the witness accumulations beside the G2 one from the
+# start or only C after it (ZKP_G2FIRST) -- every variant must give the same golden proof
 KNOBS = [{"ZKP_MSM": "seg=16"}, {"ZKP_MSM": "seg=2"}, {"ZKP_MSM": "task_w=24,task_h=48"},
          {"ZKP_MSM": "w=9,h=13"}, {"ZKP_MSM": "w=8,h=8,depth=3"}, {"ZKP_MSM": "w=20,h=20,depth=1"},
-         {"ZKP_SERIAL": "1"}]
+         {"ZKP_SERIAL": "1"}, {"ZKP_G2FIRST": "0"}, {"ZKP_G2FIRST": "3"}]
 
 
 @pytest.mark.parametrize("knobs", KNOBS, ids=lambda k: ",".join("%s=%s" % kv for kv in k.items()))

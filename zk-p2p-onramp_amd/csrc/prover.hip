@@ -337,6 +337,7 @@ class DevicePipeline {
     // priority, so they slip in between the long accumulations instead of queueing behind them
     HIPX(hipStreamCreateWithPriority(&s3_, hipStreamNonBlocking, prio_hi));
     for (auto& e : ev_) HIPX(hipEventCreate(&e));
+    HIPX(hipEventCreateWithFlags(&ev_g2acc_, hipEventDisableTiming));
     const ZkeyHeader& h = hdr_;
     const size_t nd_all = h.domain_size, c0 = (size_t)h.n_public + 1;  // first witness index with a C base
     split_range(h.n_vars, part, nparts, wlo_, whi_);
@@ -486,6 +487,7 @@ class DevicePipeline {
       if (p) (void)hipFree(p);
     if (hwin_) (void)hipHostFree(hwin_);
     for (auto& e : ev_) (void)hipEventDestroy(e);
+    if (ev_g2acc_) (void)hipEventDestroy(ev_g2acc_);
     for (int k = 0; k < NUP; ++k) {
       for (auto& t : copiers_[k]) t.reset();
       if (sup_[k]) (void)hipStreamSynchronize(sup_[k]), (void)hipStreamDestroy(sup_[k]);
@@ -839,7 +841,10 @@ class DevicePipeline {
     // s2: witness plan, then the G1 accumulations A, B1, C back to back; s3 finishes each
     // (merges + reduction: latency-bound chains) while s2 accumulates the next;
     // s1: G2 MSM B2 on the same plan; s0: quotient (buildABC, 3 coset NTTs, joinABC),
-    // H plan, H MSM.
+    // H plan, H MSM.  A starts when the G2 accumulation ends: the G2 finish (a latency-bound chain
+    // on the low-priority s1) then runs beside A, B1 and C instead of waiting out the H accumulation
+    // and sharing the proof's tail with the H finish (+0.4 %, 7 of 8 alternated pairs:
+    // profiles/g2_first_ab_r06.txt).
     // MsmPlan::build blocks its host thread once (the sort needs the nonzero-digit
     // count), so each stream is fed from its own host thread; the G2 thread starts
     // once the witness plan is enqueued (its stream then waits on plan.ready()).
@@ -848,6 +853,10 @@ class DevicePipeline {
     std::promise<void> planned;
     std::shared_future<void> planned_f = planned.get_future().share();
     bool planned_set = false;
+    const int g2first = serial_ ? 0 : g2first_;
+    std::promise<void> g2acc;
+    std::shared_future<void> g2acc_f = g2acc.get_future().share();
+    bool g2acc_set = false;
     auto g1_job = [&] {
       try {
         HIPX(hipSetDevice(dev_));
@@ -859,6 +868,10 @@ class DevicePipeline {
         planned_set = true;
         const MsmBases* tabs[3] = {ws.ta.get(), ws.tb1.get(), ws.tc.get()};
         for (int m = 0; m < 3; ++m) {
+          if (g2first && m == g2first - 1) {
+            g2acc_f.get();
+            HIPX(hipStreamWaitEvent(s2_, ev_g2acc_, 0));
+          }
           ws.g1[m]->accumulate(*ws.plan, *tabs[m]);
           HIPX(hipEventRecord(ev_[10 + m], s2_));
           HIPX(hipStreamWaitEvent(s3_, ev_[10 + m], 0));
@@ -883,10 +896,16 @@ class DevicePipeline {
         // the finish on s1 too: s3 is in-order, the G1 finishes must not queue behind it (gating the
         // G2 finish on the H plan, on either stream, measured +0.9 ms: profiles/g2_finish_r03.txt)
         ws.g2->accumulate(*ws.plan, *ws.tb2);
+        if (g2first) {
+          HIPX(hipEventRecord(ev_g2acc_, s1_));
+          g2acc.set_value();
+          g2acc_set = true;
+        }
         ws.g2->finish(*ws.plan, wb2, s1_);
         HIPX(hipEventRecord(ev_[6], s1_));
       } catch (...) {
         err[1] = std::current_exception();
+        if (g2first && !g2acc_set) g2acc.set_exception(std::current_exception());
       }
     };
     auto h_job = [&] {
@@ -971,6 +990,10 @@ class DevicePipeline {
   bool serial_ = env_int("ZKP_SERIAL", 0) == 1;  // profiling: no stream overlap
   ZkeyHeader hdr_;
   hipStream_t s0_ = nullptr, s1_ = nullptr, s2_ = nullptr, s3_ = nullptr;
+  // the G2 accumulation's end on s1: the first G1 witness accumulation (A) waits for it (g2first_ = k:
+  // accumulation k - 1 waits; ZKP_G2FIRST=0 lets A, B1, C run beside it from the start)
+  hipEvent_t ev_g2acc_ = nullptr;
+  int g2first_ = env_int("ZKP_G2FIRST", 1);
   hipEvent_t ev_[16];
   JobThread jt_g1_, jt_g2_;  // host threads feeding s2 (witness plan, G1 MSMs) and s1 (G2 MSM)
   // one witness-MSM configuration (the witness plan serves A, B1, C and B2): window bits, base tables
