@@ -13,7 +13,7 @@ import pytest
 
 PROFILES = pathlib.Path(__file__).resolve().parent.parent / "profiles"
 LINES = ["bench_r01.json", "bench_r01_recheck.json", "bench_r05_final.json", "bench_r06_a.json", "bench_r06_b.json",
-         "bench_r06_c.json"]
+         "bench_r06_c.json", "bench_r06_d.json"]
 REQUIRED = ["metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
             "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"]
 
@@ -96,7 +96,7 @@ def test_round5_line_fields():
     assert d["all_proofs_ok"] and d["cpu_baseline"]["bit_exact_vs_gpu"]
 
 
-@pytest.mark.parametrize("name", ["bench_r06_b.json", "bench_r06_c.json"])
+@pytest.mark.parametrize("name", ["bench_r06_b.json", "bench_r06_c.json", "bench_r06_d.json"])
 def test_round6_compact_line(name):
     """the driver keeps the last 8 KB of stdout, so the contract line (the LAST line)
     stays below 6,000 bytes and carries both halves of the metric (proofs/s and the 1-proof latency), the
