@@ -131,7 +131,7 @@ static int env_int(const char* name, int dflt) {
 //   w=<bits>  h=<bits>    window bits of the witness plan / the H plan and the kernel-level MSMs (8..24)
 //   depth=<rows>          base-table rows T per point (1..W; default W, or the largest depth whose
 //                         tables fit half of the free HBM)
-//   task_w=<n> task_h=<n> entries per bucket-accumulation task of either plan (default 32 / 48)
+//   task_w=<n> task_h=<n> entries per bucket-accumulation task of either plan (default 48 / 48)
 //   seg=<n>               buckets per bucket-reduction segment (a power of two; default 4)
 //   plan=dense|compact    the plan variant of the kernel-level MSMs (zkp_msm_*; default dense)
 // A malformed value or an unknown key is a ZKP_ERR_INVALID_ARG: a typo never silently tunes nothing.
@@ -212,9 +212,11 @@ static void choose_msm_params(size_t n_w, size_t n_h, const MsmOptions& o, MsmPa
   // H-plan tasks of <= 48 entries (the uniform quotient scalars fill every bucket evenly, ~208 entries at
   // the Venmo shape: 5 task partials per bucket instead of 7, so the latency-bound merge_final at the end
   // of the proof folds fewer): +0.7 % and +0.9 % proofs/s over 32, 7 of 7 alternated rounds on two boxes
-  // (profiles/task_size_ab_r05.txt); the witness plan keeps 32 (its 0/1-heavy buckets: 24-64 within noise)
+  // (profiles/task_size_ab_r05.txt).  Witness-plan tasks of <= 48 too since the G2 accumulation runs first
+  // (round 6): +0.6 / +1.0 % over 32 on two boxes, every alternated pair; 96 ties, 128 and 192 lose
+  // (profiles/task_w_ab_r06.txt)
   auto tune = [&] {
-    if (o.task_w > 0) pw.S = o.task_w;
+    pw.S = o.task_w > 0 ? o.task_w : 48;
     ph.S = o.task_h > 0 ? o.task_h : 48;
     for (MsmParams* q : {&pw, &ph})
       if (o.seg > 0 && o.seg <= (1 << (q->c - 1))) q->M = o.seg;
@@ -394,7 +396,7 @@ class DevicePipeline {
         const MsmParams p2 = make_params(nv, c2, 0);
         if ((size_t)p2.windows * nv * (3 * 64 + 128) <= free_b / 2) {
           ws_[1].pw = make_params(nv, c2, p2.windows);
-          if (opt.task_w > 0) ws_[1].pw.S = opt.task_w;
+          ws_[1].pw.S = opt.task_w > 0 ? opt.task_w : 48;
           if (opt.seg > 0 && opt.seg <= (1 << (ws_[1].pw.c - 1))) ws_[1].pw.M = opt.seg;
           build_wtables(ws_[1]);
           nws_ = 2;
