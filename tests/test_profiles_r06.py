@@ -98,7 +98,7 @@ def test_proof_valu_r06_recomputes(tmp_path):
     out = tmp_path / "pv.json"
     subprocess.run([sys.executable, os.path.join(ROOT, "tools", "prof", "proof_valu.py"),
                     os.path.join(ROOT, "profiles", "proof_valu_r06", "valu_counter_collection.csv"),
-                    os.path.join(ROOT, "profiles", "bench_r06_c.json"), str(out)],
+                    os.path.join(ROOT, "profiles", "bench_r06_d.json"), str(out)],
                    check=True, capture_output=True, timeout=120)
     got = json.load(open(out))
     want = json.load(open(os.path.join(ROOT, "profiles", "proof_valu_r06.json")))

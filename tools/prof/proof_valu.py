@@ -10,8 +10,8 @@ counts do not depend on concurrency.  Per proof and per kernel class:
 and the sum of the dispatches' serialised times.  Against the bench's concurrent ms per proof this says how
 much of a proof's span the VALU work fills.
 usage: proof_valu.py <run_counter_collection.csv> <bench line json> [out.json]
-(round 6: tools/gpu/pmc.sh pw valu, three whole proofs kept in profiles/proof_valu_r06/, the span from
-profiles/bench_r06_c.json -> profiles/proof_valu_r06.json)"""
+(round 6: tools/gpu/pmc.sh pw2 valu on the final library, three whole proofs kept in profiles/proof_valu_r06/,
+the span from profiles/bench_r06_d.json -> profiles/proof_valu_r06.json)"""
 import collections
 import csv
 import json
